@@ -1,0 +1,248 @@
+/*
+ * gpu_actor.h — C-ABI of the MI355X actor-dispatch engine (libgpuactor.so).
+ *
+ * Drop-in boundary for the Pony runtime's data-parallel hot path: the entry
+ * points below replace, for GPU-resident POD-state actors, the pony.h calls a
+ * compiled Pony program makes on that path. Actors are
+ * addressed by 32-bit ids instead of pony_actor_t*, state is plain words,
+ * and behaviours come from a fixed table of device handlers (the analogue of
+ * pony_type_t.dispatch, pony.h:114-115,171-195).
+ *
+ * Conventions mirrored from pony.h:
+ *   - ownership of a message passes to the library at send (pony_sendv,
+ *     pony.h:271-279); messages in one gpu_actor_sendv call keep their order
+ *     (a pony_chain, pony.h:296-305);
+ *   - per-sender->receiver FIFO and causal delivery (the guarantee
+ *     codegen_optimisation.cc:13-41 pins) hold;
+ *   - unlike pony.h, errors are returned as codes (0 ok, <0 error), never
+ *     raised, so every entry point is safe to declare as Pony FFI without `?`;
+ *   - calls from different host threads are serialised internally.
+ *
+ * Execution model: bulk-synchronous supersteps. In step s every actor with
+ * pending mail drains up to `batch` messages (PONY_SCHED_BATCH = 100,
+ * actor.c:20, overridable per type like the fork's _batch() hint,
+ * pony.h:156-162) and runs the handler for each; messages sent in step s are
+ * delivered from step s+1 on. Each step's arrivals at an actor are delivered
+ * in (sender id, sender sequence) order, after any carried-over mail; host
+ * sends count as senders with ids above every actor id.
+ */
+#ifndef GPU_ACTOR_H
+#define GPU_ACTOR_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#if defined(__cplusplus)
+extern "C" {
+#endif
+
+#define GPU_ACTOR_API __attribute__((visibility("default")))
+
+/* ---- error codes ------------------------------------------------------- */
+#define GPU_ACTOR_OK            0
+#define GPU_ACTOR_EINVAL       -1   /* bad argument / unknown type / bad id   */
+#define GPU_ACTOR_ENOMEM       -2   /* device or host allocation failed        */
+#define GPU_ACTOR_ENODEV       -3   /* no usable GPU                           */
+#define GPU_ACTOR_EMAILBOX     -4   /* a mailbox overflowed; messages dropped  */
+#define GPU_ACTOR_EHIP         -5   /* HIP runtime error                       */
+#define GPU_ACTOR_ESTATE       -6   /* not initialised / already initialised   */
+#define GPU_ACTOR_ERANGE       -7   /* sequence or id space exhausted          */
+#define GPU_ACTOR_ECOMM        -8   /* RCCL / exchange failure                 */
+
+#define GPU_ACTOR_MAX_TYPES    16
+#define GPU_ACTOR_MAX_PARAMS   8
+
+/* ---- messages ------------------------------------------------------------ */
+/* One application message: the POD analogue of pony_msgi_t (pony.h:53-58). */
+typedef struct gpu_msg_t
+{
+  uint32_t to;          /* receiver actor id                           */
+  uint32_t behaviour;   /* behaviour index within the receiver's table */
+  uint64_t arg;         /* the single machine-word argument            */
+} gpu_msg_t;
+
+/* ---- configuration ------------------------------------------------------ */
+typedef struct gpu_actor_config_t
+{
+  int32_t  device;          /* HIP device ordinal for this process (-1: current)  */
+  uint32_t n_ranks;         /* processes (one per GPU) sharing the actor space   */
+  uint32_t rank;            /* this process's rank, 0 <= rank < n_ranks          */
+  uint32_t batch;           /* default per-step drain limit (0 -> 100)           */
+  uint32_t mailbox_cap;     /* default mailbox ring capacity, power of 2 (0->64) */
+  uint32_t max_exchange;    /* per-peer records per step for n_ranks>1 (0->auto) */
+  uint64_t max_actors;      /* capacity of the global id space (0 -> 1<<26)      */
+  const void* comm_id;      /* 128-byte ncclUniqueId from rank 0 (n_ranks > 1)  */
+} gpu_actor_config_t;
+
+/* Counters read back by gpu_actor_counts (device-side counters, summed over
+ * ranks when n_ranks > 1). */
+typedef struct gpu_actor_counts_t
+{
+  uint64_t steps;       /* supersteps run since init                        */
+  uint64_t delivered;   /* application messages handled (handler invocations) */
+  uint64_t sent;        /* application messages emitted by handlers          */
+  uint64_t pending;     /* messages waiting in mailboxes now                 */
+  uint64_t dropped;     /* messages lost to mailbox overflow (error)          */
+  uint64_t remote;      /* messages that crossed ranks                       */
+  uint64_t delivered_by_type[GPU_ACTOR_MAX_TYPES];
+} gpu_actor_counts_t;
+
+/* ---- lifecycle (pony_init / pony_start / pony_stop, pony.h:486-559) ------ */
+GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg);
+GPU_ACTOR_API int gpu_actor_shutdown(void);
+/* 128-byte communicator id to broadcast from rank 0 before gpu_actor_init. */
+GPU_ACTOR_API int gpu_actor_comm_id(void* out128);
+
+/* ---- types (pony_type_t, pony.h:171-195) -------------------------------- */
+/* Register actor type `type_id` (< GPU_ACTOR_MAX_TYPES) with `state_words`
+ * 64-bit words of POD state, dispatching to handler table `handler_table`
+ * (GPU_ACTOR_HT_*). */
+GPU_ACTOR_API int gpu_actor_type_register(uint32_t type_id, uint32_t state_words,
+  uint32_t handler_table);
+/* Per-type drain limit (the fork's _batch() hint, actor.c:410-416) and mailbox
+ * ring capacity (power of two). 0 keeps the config default. */
+GPU_ACTOR_API int gpu_actor_type_config(uint32_t type_id, uint32_t batch,
+  uint32_t mailbox_cap);
+/* Handler-table parameter `idx` (< GPU_ACTOR_MAX_PARAMS) of a type; set before
+ * gpu_actor_create, which runs the table's constructor with them. */
+GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
+
+/* ---- actors (pony_create, actor.c:688-734) ------------------------------ */
+/* Bulk-create `count` actors of a type (once per type); ids are
+ * [*first_id, *first_id + count). Runs the table's constructor on device. */
+GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* first_id);
+
+/* ---- sending from the host (pony_alloc_msg + pony_sendv, actor.c:749-817) */
+/* Host staging buffer for up to n messages, owned by the library and valid
+ * until the next gpu_actor_alloc_msgs / gpu_actor_shutdown. */
+GPU_ACTOR_API int gpu_actor_alloc_msgs(uint64_t n, gpu_msg_t** buf);
+/* Send n messages in order (a chain). Ownership passes to the library. */
+GPU_ACTOR_API int gpu_actor_sendv(const gpu_msg_t* first, uint64_t n);
+/* pony_sendi (actor.c:959-968) analogue. */
+GPU_ACTOR_API int gpu_actor_send(uint64_t to, uint32_t behaviour, uint64_t arg);
+
+/* ---- running (the scheduler run loop, scheduler.c:953-1090) ------------- */
+/* Run up to max_steps supersteps (0: until quiescent, i.e. no pending mail on
+ * any rank). *steps_done receives the number of steps that handled mail. */
+GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done);
+/* Run exactly n supersteps without any host synchronisation between them
+ * (benchmark form: no quiescence test, no readback). */
+GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n);
+/* Block until all queued device work is done; returns the sticky error. */
+GPU_ACTOR_API int gpu_actor_sync(void);
+
+/* ---- state and counters ------------------------------------------------- */
+/* Copy state of actors [first, first+n) of a type (indices relative to the
+ * type's first id; only actors owned by this rank are meaningful when
+ * n_ranks > 1). Layout: field-major, out[w * n + i] = word w of actor i. */
+GPU_ACTOR_API int gpu_actor_state_read(uint32_t type_id, uint64_t first, uint64_t n,
+  uint64_t* out);
+GPU_ACTOR_API int gpu_actor_state_write(uint32_t type_id, uint64_t first, uint64_t n,
+  const uint64_t* in);
+GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out);
+/* Id of the rank owning actor `id` (hash partition; id % n_ranks). */
+GPU_ACTOR_API uint32_t gpu_actor_owner(uint64_t id);
+/* Device stream the engine runs on (hipStream_t), for profiling/overlap. */
+GPU_ACTOR_API void* gpu_actor_stream(void);
+/* Average duration (ms) of the drain kernel over the last gpu_actor_run_fixed,
+ * measured with HIP events on the engine's stream; 0 if unavailable. */
+GPU_ACTOR_API double gpu_actor_last_drain_ms(void);
+GPU_ACTOR_API const char* gpu_actor_strerror(int code);
+
+/* ======================================================================== */
+/* Fixed handler tables. Each table is the device restatement of one         */
+/* reference actor's behaviours. Behaviour ids, state words and params:     */
+/* ======================================================================== */
+
+/* Ring (examples/ring/main.pony:3-24).
+ *   state: [0] next (actor id; ~0 = None)  [1] ring id (1..size)
+ *          [2] pass messages received        [3] pass(0) received ("print")
+ *   params: [0] ring size (constructor: actor k of ring j gets id k%size+1,
+ *           next = the actor with id+1, except id 1 whose next comes by set)
+ *   behaviours: SET(arg = neighbour id), PASS(arg = i)                      */
+#define GPU_ACTOR_HT_RING            1
+#define GPU_ACTOR_RING_SET           0
+#define GPU_ACTOR_RING_PASS          1
+
+/* Pinger of examples/message-ubench/main.pony:229-286 with a per-pinger
+ * forward budget in place of the wall-clock interval. Rand is seeded
+ * Rand(seed + i + 1, 0x9E3779B97F4A7C15) and primed with three int(100).
+ *   state: [0] rng x  [1] rng y  [2] pings received
+ *   params: [0] N pingers  [1] first pinger id  [2] budget  [3] seed
+ *   behaviours: PING(arg): count += 1; if count <= budget:
+ *               ping(42) to pinger rand.int(N)                               */
+#define GPU_ACTOR_HT_PINGER          2
+#define GPU_ACTOR_PINGER_PING        0
+
+/* message-ubench-det: a token's route depends only on its
+ * payload. arg = token << 32 | hop.
+ *   state: [0] pings received  [1] xor of payloads
+ *   params: [0] N  [1] first id  [2] hops H  [3] seed
+ *   behaviours: PING(arg): count++, acc ^= arg; if hop < H: send
+ *               (token<<32 | hop+1) to first + mulhi(splitmix64(seed^arg), N) */
+#define GPU_ACTOR_HT_PINGER_DET      3
+#define GPU_ACTOR_PINGER_DET_PING    0
+
+/* fan-in Sender (examples/fan-in/main.pony:231-254), P messages each.
+ *   state: [0] rng x [1] rng y [2] remaining [3] sent
+ *   params: [0] analyzers A [1] first analyzer id [2] P
+ *           [3] seed mode (0: every sender Rand() = Rand(5489, 0) as in the
+ *               reference, fan-in/main.pony:235; 1: Rand(5489 + i, 0))
+ *   behaviours: SEND_MSGS: MSG(i << 32 | sent) to analyzer
+ *               rand.int_unbiased(A); sent++; if --remaining: SEND_MSGS to self */
+#define GPU_ACTOR_HT_FANIN_SENDER    4
+#define GPU_ACTOR_FANIN_SEND_MSGS    0
+
+/* fan-in Analyzer (fan-in/main.pony:212-229). Commutative ("reducible"):
+ * messages are applied as device atomics when sent.
+ *   state: [0] messages received  [1] xor of args
+ *   behaviours: MSG(arg)                                                     */
+#define GPU_ACTOR_HT_FANIN_ANALYZER  5
+#define GPU_ACTOR_FANIN_MSG          0
+
+/* gups Streamer (examples/gups_basic/main.pony:93-143), one message per
+ * update. Streamer i uses PolyRand(i * stride).
+ *   state: [0] PolyRand last  [1] finished flag
+ *   params: [0] chunk [1] shift [2] updater mask [3] first updater id
+ *           [4] unused [5] seed stride
+ *   behaviours: APPLY(iterate): chunk x UPDATE(d) to updater (d>>shift)&mask;
+ *               if iterate > 0: APPLY(iterate-1) to self else finished = 1   */
+#define GPU_ACTOR_HT_GUPS_STREAMER   6
+#define GPU_ACTOR_GUPS_APPLY         0
+
+/* gups Updater (gups_basic/main.pony:145-165). Reducible (XOR).
+ *   state: `size` words, table[k] = k + index*size initially
+ *   params: [0] size (power of two)
+ *   behaviours: UPDATE(d): table[d & (size-1)] ^= d                           */
+#define GPU_ACTOR_HT_GUPS_UPDATER    7
+#define GPU_ACTOR_GUPS_UPDATE        0
+
+/* Message storm: a ring token plus random-target traffic.
+ *   state: [0] messages received  [1] xor of args
+ *   params: [0] N [1] first id [2] hops H [3] seed
+ *   behaviours: TOKEN(hop): count++, acc ^= hop; if hop < H: TOKEN(hop+1)
+ *               to the next actor (wrapping); STORM(arg): as PINGER_DET.PING */
+#define GPU_ACTOR_HT_STORM           8
+#define GPU_ACTOR_STORM_TOKEN        0
+#define GPU_ACTOR_STORM_STORM        1
+
+/* Per-pair FIFO probe (order-sensitive; codegen_optimisation.cc:13-41).
+ * Source i targets sink first_sink + i % n_sinks.
+ *   FIFO_SRC state: [0] target [1] seq [2] bursts left
+ *            params: [0] first sink id [1] n sinks [2] bursts
+ *            BURST(m): m x PUSH(i << 32 | ++seq); if --bursts: BURST(m) to self
+ *   FIFO_SINK state: [0] h (FNV-1a fold of args, order-sensitive) [1] n
+ *            [2] FIFO violations [3..10] last seq per source slot
+ *            params: [0] n sinks
+ *            PUSH(arg): slot = ((arg >> 32) / n_sinks) % 8                   */
+#define GPU_ACTOR_HT_FIFO_SRC        9
+#define GPU_ACTOR_FIFO_BURST         0
+#define GPU_ACTOR_HT_FIFO_SINK       10
+#define GPU_ACTOR_FIFO_PUSH          0
+
+#define GPU_ACTOR_NONE 0xFFFFFFFFFFFFFFFFULL
+
+#if defined(__cplusplus)
+}
+#endif
+#endif

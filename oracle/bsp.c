@@ -1,0 +1,479 @@
+/*
+ * bsp.c — TEST INFRASTRUCTURE ONLY: single-threaded bulk-synchronous
+ * restatement of the gpu_actor engine semantics (include/gpu_actor.h), used by
+ * tests/ as the parity checker for the HIP engine. Written independently of
+ * ponyc_amd/csrc: it restates the reference behaviours (file:line cited at each
+ * handler) over the engine's delivery rules:
+ *
+ *   - step s visits actors in ascending id order (the canonical order);
+ *   - an actor handles min(batch, mail pending at the start of s) messages
+ *     from the head of its mailbox (actor.c:437-471, batch = PONY_SCHED_BATCH
+ *     actor.c:20 or the per-type override, actor.c:410-416);
+ *   - an emitted message is appended to the receiver's mailbox and is first
+ *     visible in step s+1; so each step's arrivals are ordered by
+ *     (sender id, sender sequence), after carried-over mail;
+ *   - a message whose append would take the mailbox past `cap` slots beyond
+ *     the head at the start of the step is dropped and counted;
+ *   - messages to "reducible" types (all behaviours commutative) are applied
+ *     when sent;
+ *   - host sends are appended in call order (ids above every actor).
+ *
+ * Not thread-safe; one simulator per process.
+ */
+#include "oracle.h"
+#include "../include/gpu_actor.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { uint32_t beh; uint64_t arg; } orec_t;
+
+typedef struct {
+  orec_t*  buf;
+  uint64_t cap_alloc;
+  uint64_t head;          /* index of next message to handle (absolute)     */
+  uint64_t tail;          /* number of messages ever appended (absolute)     */
+  uint64_t head_start;    /* head at the start of the current step / window  */
+} mbox_t;
+
+typedef struct {
+  int      registered, created;
+  uint32_t words, ht, batch, cap, reducible;
+  uint64_t params[GPU_ACTOR_MAX_PARAMS];
+  uint64_t first, count;
+  uint64_t* state;        /* field-major: state[w * count + i] */
+  uint64_t delivered;
+} otype_t;
+
+static struct {
+  int       init;
+  otype_t   types[GPU_ACTOR_MAX_TYPES];
+  uint64_t  n_actors;
+  uint8_t*  type_of;      /* actor id -> type id */
+  mbox_t*   mb;
+  uint64_t  steps, delivered, sent, dropped;
+} S;
+
+static const uint32_t DEFAULT_BATCH = 100;   /* PONY_SCHED_BATCH, actor.c:20 */
+static const uint32_t DEFAULT_CAP = 64;
+
+static int ht_reducible(uint32_t ht)
+{
+  return ht == GPU_ACTOR_HT_FANIN_ANALYZER || ht == GPU_ACTOR_HT_GUPS_UPDATER;
+}
+
+int or_init(uint32_t n_types_max)
+{
+  (void)n_types_max;
+  if(S.init) or_shutdown();
+  memset(&S, 0, sizeof(S));
+  S.init = 1;
+  return 0;
+}
+
+void or_shutdown(void)
+{
+  for(int t = 0; t < GPU_ACTOR_MAX_TYPES; t++)
+    free(S.types[t].state);
+  for(uint64_t a = 0; a < S.n_actors; a++)
+    free(S.mb[a].buf);
+  free(S.mb);
+  free(S.type_of);
+  memset(&S, 0, sizeof(S));
+}
+
+int or_type_register(uint32_t type_id, uint32_t state_words, uint32_t ht)
+{
+  if(!S.init || type_id >= GPU_ACTOR_MAX_TYPES || ht < 1 || ht > 10) return GPU_ACTOR_EINVAL;
+  otype_t* t = &S.types[type_id];
+  if(t->registered) return GPU_ACTOR_EINVAL;
+  t->registered = 1;
+  t->words = state_words;
+  t->ht = ht;
+  t->batch = DEFAULT_BATCH;
+  t->cap = DEFAULT_CAP;
+  t->reducible = (uint32_t)ht_reducible(ht);
+  return 0;
+}
+
+int or_type_config(uint32_t type_id, uint32_t batch, uint32_t cap)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered) return GPU_ACTOR_EINVAL;
+  if(batch) S.types[type_id].batch = batch;
+  if(cap) S.types[type_id].cap = cap;
+  return 0;
+}
+
+int or_type_param(uint32_t type_id, uint32_t idx, uint64_t value)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || idx >= GPU_ACTOR_MAX_PARAMS ||
+    !S.types[type_id].registered) return GPU_ACTOR_EINVAL;
+  S.types[type_id].params[idx] = value;
+  return 0;
+}
+
+/* ---- constructors (the reference `new create`) --------------------------- */
+static void construct(uint32_t tid)
+{
+  otype_t* t = &S.types[tid];
+  uint64_t n = t->count;
+  uint64_t* st = t->state;
+  for(uint64_t i = 0; i < n; i++)
+  {
+    switch(t->ht)
+    {
+      case GPU_ACTOR_HT_RING: {
+        /* ring/main.pony:61-72: Ring(1) first, then Ring(size-k) whose
+         * neighbour is the previously created actor; id m -> id m+1 -> ... */
+        uint64_t size = t->params[0] ? t->params[0] : 1;
+        uint64_t ring = i / size, p = i % size;
+        st[0 * n + i] = (p == 0) ? GPU_ACTOR_NONE : t->first + ring * size + (p + 1) % size;
+        st[1 * n + i] = p + 1;
+        break;
+      }
+      case GPU_ACTOR_HT_PINGER: {
+        /* message-ubench/main.pony:244-249 with a seeded Rand. */
+        or_xoro_t r;
+        or_xoro_create(&r, t->params[3] + i + 1, 0x9E3779B97F4A7C15ULL);
+        (void)or_rand_int(&r, 100); (void)or_rand_int(&r, 100); (void)or_rand_int(&r, 100);
+        st[0 * n + i] = r.x; st[1 * n + i] = r.y;
+        break;
+      }
+      case GPU_ACTOR_HT_FANIN_SENDER: {
+        /* fan-in/main.pony:235: `let _rand: Rand = Rand()` -> Rand(5489, 0). */
+        or_xoro_t r;
+        or_xoro_create(&r, t->params[3] ? 5489 + i : 5489, 0);
+        st[0 * n + i] = r.x; st[1 * n + i] = r.y;
+        st[2 * n + i] = t->params[2];
+        break;
+      }
+      case GPU_ACTOR_HT_GUPS_STREAMER: {
+        or_polyrand_t pr;
+        or_polyrand_create(&pr, t->params[5] * i);
+        st[0 * n + i] = pr.last;
+        break;
+      }
+      case GPU_ACTOR_HT_GUPS_UPDATER: {
+        /* gups_basic/main.pony:148-155: table[k] = k + index*size. */
+        uint64_t size = t->params[0];
+        for(uint64_t k = 0; k < size && k < t->words; k++)
+          st[k * n + i] = k + i * size;
+        break;
+      }
+      case GPU_ACTOR_HT_FIFO_SRC: {
+        uint64_t ns = t->params[1] ? t->params[1] : 1;
+        st[0 * n + i] = t->params[0] + i % ns;
+        st[2 * n + i] = t->params[2];
+        break;
+      }
+      case GPU_ACTOR_HT_FIFO_SINK:
+        st[0 * n + i] = 0xcbf29ce484222325ULL;
+        break;
+      default:
+        break;
+    }
+  }
+}
+
+int or_create(uint32_t type_id, uint64_t count, uint64_t* first_id)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
+  otype_t* t = &S.types[type_id];
+  if(!t->registered || t->created) return GPU_ACTOR_EINVAL;
+  uint64_t total = S.n_actors + count;
+  uint8_t* to = realloc(S.type_of, total ? total : 1);
+  mbox_t* mb = realloc(S.mb, (total ? total : 1) * sizeof(mbox_t));
+  if(!to || !mb) return GPU_ACTOR_ENOMEM;
+  S.type_of = to; S.mb = mb;
+  for(uint64_t a = S.n_actors; a < total; a++)
+  {
+    S.type_of[a] = (uint8_t)type_id;
+    memset(&S.mb[a], 0, sizeof(mbox_t));
+  }
+  t->first = S.n_actors;
+  t->count = count;
+  t->state = calloc(t->words * count + 1, sizeof(uint64_t));
+  if(!t->state) return GPU_ACTOR_ENOMEM;
+  t->created = 1;
+  S.n_actors = total;
+  construct(type_id);
+  if(first_id) *first_id = t->first;
+  return 0;
+}
+
+/* ---- delivery ------------------------------------------------------------ */
+static void apply_reducible(otype_t* t, uint64_t i, uint32_t beh, uint64_t arg)
+{
+  uint64_t n = t->count;
+  switch(t->ht)
+  {
+    case GPU_ACTOR_HT_FANIN_ANALYZER:
+      /* Analyzer.msg_from_sender (fan-in/main.pony:219-220): count += 1. */
+      t->state[0 * n + i] += 1;
+      t->state[1 * n + i] ^= arg;
+      break;
+    case GPU_ACTOR_HT_GUPS_UPDATER: {
+      /* Updater.apply (gups_basic/main.pony:157-162). */
+      uint64_t size = t->params[0];
+      uint64_t k = arg & (size - 1);
+      t->state[k * n + i] ^= arg;
+      break;
+    }
+  }
+  (void)beh;
+  t->delivered++;
+  S.delivered++;
+}
+
+static void deliver(uint64_t to, uint32_t beh, uint64_t arg)
+{
+  if(to >= S.n_actors) { S.dropped++; return; }
+  otype_t* t = &S.types[S.type_of[to]];
+  if(t->reducible)
+  {
+    apply_reducible(t, to - t->first, beh, arg);
+    return;
+  }
+  mbox_t* m = &S.mb[to];
+  if(m->tail - m->head_start >= t->cap) { S.dropped++; return; }
+  if(m->tail - m->head >= m->cap_alloc)
+  {
+    uint64_t nc = m->cap_alloc ? m->cap_alloc * 2 : 8;
+    orec_t* nb = malloc(nc * sizeof(orec_t));
+    for(uint64_t k = m->head; k < m->tail; k++)
+      nb[k % nc] = m->buf[k % m->cap_alloc];
+    free(m->buf);
+    m->buf = nb;
+    m->cap_alloc = nc;
+  }
+  m->buf[m->tail % m->cap_alloc].beh = beh;
+  m->buf[m->tail % m->cap_alloc].arg = arg;
+  m->tail++;
+}
+
+static void send(uint64_t to, uint32_t beh, uint64_t arg)
+{
+  S.sent++;
+  deliver(to, beh, arg);
+}
+
+int or_send(uint64_t to, uint32_t behaviour, uint64_t arg)
+{
+  if(!S.init) return GPU_ACTOR_ESTATE;
+  if(to >= S.n_actors) return GPU_ACTOR_EINVAL;
+  deliver(to, behaviour, arg);
+  return 0;
+}
+
+int or_sendv(const void* msgs, uint64_t n)
+{
+  const gpu_msg_t* m = (const gpu_msg_t*)msgs;
+  for(uint64_t k = 0; k < n; k++)
+  {
+    int rc = or_send(m[k].to, m[k].behaviour, m[k].arg);
+    if(rc) return rc;
+  }
+  return 0;
+}
+
+/* ---- behaviours ---------------------------------------------------------- */
+static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
+{
+  uint64_t n = t->count, i = self - t->first;
+  uint64_t* st = t->state;
+#define W(k) st[(uint64_t)(k) * n + i]
+  switch(t->ht)
+  {
+    case GPU_ACTOR_HT_RING:
+      if(beh == GPU_ACTOR_RING_SET)
+      {
+        W(0) = arg;                                 /* ring/main.pony:13-14 */
+      } else {
+        W(2) += 1;                                  /* ring/main.pony:16-24 */
+        if(arg > 0)
+        {
+          if(W(0) != GPU_ACTOR_NONE)
+            send(W(0), GPU_ACTOR_RING_PASS, arg - 1);
+        } else {
+          W(3) += 1;                                /* _env.out.print(_id)  */
+        }
+      }
+      break;
+
+    case GPU_ACTOR_HT_PINGER: {
+      /* message-ubench/main.pony:265-286 (ping + send_pings). */
+      or_xoro_t r = { W(0), W(1) };
+      W(2) += 1;
+      if(W(2) <= t->params[2])
+      {
+        uint64_t k = or_rand_int(&r, t->params[0]);
+        send(t->params[1] + k, GPU_ACTOR_PINGER_PING, 42);
+      }
+      W(0) = r.x; W(1) = r.y;
+      break;
+    }
+
+    case GPU_ACTOR_HT_PINGER_DET:
+    case GPU_ACTOR_HT_STORM: {
+      W(0) += 1;
+      if(t->ht == GPU_ACTOR_HT_STORM && beh == GPU_ACTOR_STORM_TOKEN)
+      {
+        W(1) ^= arg;
+        if(arg < t->params[2])
+        {
+          uint64_t nxt = (i + 1 == n) ? t->first : self + 1;
+          send(nxt, GPU_ACTOR_STORM_TOKEN, arg + 1);
+        }
+        break;
+      }
+      W(1) ^= arg;
+      uint64_t hop = arg & 0xFFFFFFFFULL;
+      if(hop < t->params[2])
+      {
+        uint64_t k = or_mulhi(or_splitmix_mix(t->params[3] ^ arg), t->params[0]);
+        send(t->params[1] + k, beh, (arg & 0xFFFFFFFF00000000ULL) | (hop + 1));
+      }
+      break;
+    }
+
+    case GPU_ACTOR_HT_FANIN_SENDER: {
+      /* Sender.send_msgs (fan-in/main.pony:241-250). */
+      or_xoro_t r = { W(0), W(1) };
+      uint64_t k = or_rand_int_unbiased(&r, t->params[0]);
+      send(t->params[1] + k, GPU_ACTOR_FANIN_MSG, (i << 32) | W(3));
+      W(3) += 1;
+      W(0) = r.x; W(1) = r.y;
+      if(W(2) > 0) W(2) -= 1;
+      if(W(2) > 0)
+        send(self, GPU_ACTOR_FANIN_SEND_MSGS, 0);
+      break;
+    }
+
+    case GPU_ACTOR_HT_GUPS_STREAMER: {
+      /* Streamer.apply (gups_basic/main.pony:110-143), one message per datum. */
+      or_polyrand_t pr = { W(0) };
+      uint64_t chunk = t->params[0], shift = t->params[1], mask = t->params[2];
+      for(uint64_t c = 0; c < chunk; c++)
+      {
+        uint64_t d = or_polyrand_next(&pr);
+        uint64_t u = (d >> shift) & mask;
+        send(t->params[3] + u, GPU_ACTOR_GUPS_UPDATE, d);
+      }
+      W(0) = pr.last;
+      if(arg > 0)
+        send(self, GPU_ACTOR_GUPS_APPLY, arg - 1);
+      else
+        W(1) = 1;                                  /* main.streamer_done() */
+      break;
+    }
+
+    case GPU_ACTOR_HT_FIFO_SRC: {
+      for(uint64_t j = 0; j < arg; j++)
+      {
+        W(1) += 1;
+        send(W(0), GPU_ACTOR_FIFO_PUSH, (i << 32) | W(1));
+      }
+      if(W(2) > 0) W(2) -= 1;
+      if(W(2) > 0)
+        send(self, GPU_ACTOR_FIFO_BURST, arg);
+      break;
+    }
+
+    case GPU_ACTOR_HT_FIFO_SINK: {
+      uint64_t ns = t->params[0] ? t->params[0] : 1;
+      uint64_t slot = ((arg >> 32) / ns) % 8;
+      uint64_t seq = arg & 0xFFFFFFFFULL;
+      W(1) += 1;
+      W(0) = (W(0) ^ arg) * 0x100000001b3ULL;
+      if(seq != W(3 + slot) + 1) W(2) += 1;
+      W(3 + slot) = seq;
+      break;
+    }
+  }
+#undef W
+}
+
+/* ---- run ----------------------------------------------------------------- */
+static uint64_t pending_total(void)
+{
+  uint64_t p = 0;
+  for(uint64_t a = 0; a < S.n_actors; a++)
+    p += S.mb[a].tail - S.mb[a].head;
+  return p;
+}
+
+int or_run(uint64_t max_steps, uint64_t* steps_done)
+{
+  if(!S.init) return GPU_ACTOR_ESTATE;
+  uint64_t done = 0;
+  uint64_t* avail = malloc((S.n_actors ? S.n_actors : 1) * sizeof(uint64_t));
+  if(!avail) return GPU_ACTOR_ENOMEM;
+  while((max_steps == 0 || done < max_steps) && pending_total() > 0)
+  {
+    for(uint64_t a = 0; a < S.n_actors; a++)
+    {
+      S.mb[a].head_start = S.mb[a].head;
+      avail[a] = S.mb[a].tail - S.mb[a].head;
+    }
+    for(uint64_t a = 0; a < S.n_actors; a++)
+    {
+      if(avail[a] == 0) continue;
+      otype_t* t = &S.types[S.type_of[a]];
+      uint64_t w = avail[a] < t->batch ? avail[a] : t->batch;
+      mbox_t* m = &S.mb[a];
+      for(uint64_t k = 0; k < w; k++)
+      {
+        orec_t r = m->buf[m->head % m->cap_alloc];
+        m->head++;
+        t->delivered++;
+        S.delivered++;
+        handle(t, a, r.beh, r.arg);
+      }
+    }
+    /* the window for host sends after this step starts at the new head */
+    for(uint64_t a = 0; a < S.n_actors; a++)
+      S.mb[a].head_start = S.mb[a].head;
+    done++;
+  }
+  free(avail);
+  S.steps += done;
+  if(steps_done) *steps_done = done;
+  return S.dropped ? GPU_ACTOR_EMAILBOX : 0;
+}
+
+int or_state_read(uint32_t type_id, uint64_t first, uint64_t n, uint64_t* out)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
+  otype_t* t = &S.types[type_id];
+  if(!t->created || first + n > t->count) return GPU_ACTOR_EINVAL;
+  for(uint32_t w = 0; w < t->words; w++)
+    memcpy(out + (uint64_t)w * n, t->state + (uint64_t)w * t->count + first, n * sizeof(uint64_t));
+  return 0;
+}
+
+int or_state_write(uint32_t type_id, uint64_t first, uint64_t n, const uint64_t* in)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
+  otype_t* t = &S.types[type_id];
+  if(!t->created || first + n > t->count) return GPU_ACTOR_EINVAL;
+  for(uint32_t w = 0; w < t->words; w++)
+    memcpy(t->state + (uint64_t)w * t->count + first, in + (uint64_t)w * n, n * sizeof(uint64_t));
+  return 0;
+}
+
+int or_counts(uint64_t* out)
+{
+  out[0] = S.steps;
+  out[1] = S.delivered;
+  out[2] = S.sent;
+  out[3] = pending_total();
+  out[4] = S.dropped;
+  return 0;
+}
+
+int or_type_delivered(uint32_t type_id, uint64_t* out)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
+  *out = S.types[type_id].delivered;
+  return 0;
+}

@@ -1,0 +1,118 @@
+/*
+ * harness/ubench.c — TEST INFRASTRUCTURE ONLY. examples/message-ubench Pingers
+ * on the reference runtime, with the workload made deterministic:
+ *   --det 0 : faithful Pinger.ping/send_pings (message-ubench/main.pony:265-286)
+ *             with a seeded Rand(seed+i+1, 0x9E3779B97F4A7C15) primed by three
+ *             int(100) (main.pony:244-249) and a per-pinger forward budget B
+ *             in place of the timer. Every ping is identical, so a pinger's
+ *             state is a function of how many pings it has received: the
+ *             network is abelian and its final state is schedule-independent.
+ *   --det 1 : message-ubench-det: token<<32|hop payloads routed
+ *             by splitmix64(seed ^ payload), H hops.
+ * SyncLeader's role (tell_all_to_go, main.pony:201-218) is played by main():
+ * each pinger receives I initial pings. Usage:
+ *   harness_ubench --pingers N --initial I [--budget B | --det 1 --hops H]
+ *                  [--seed S] [--threads T] [--out file]
+ * Output (field-major u64): faithful: x, y, count; det: count, acc.
+ */
+#include "harness.h"
+
+enum { PING = 0 };
+
+typedef struct pinger_t {
+  pony_actor_pad_t pad;
+  or_xoro_t rand;          /* _rand */
+  uint64_t count;          /* _count */
+  uint64_t acc;
+  uint64_t idx;
+} pinger_t;
+
+static pinger_t** g_ps;    /* _ps */
+static uint64_t g_n, g_budget, g_hops, g_seed;
+static int g_det;
+static uint64_t *g_x, *g_y, *g_count, *g_acc;
+
+static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
+{
+  pinger_t* p = (pinger_t*)self;
+  uint64_t payload = (uint64_t)((pony_msgi_t*)m)->i;
+  if(!g_det)
+  {
+    /* be ping(payload): _count = _count + 1; send_pings() while in budget */
+    p->count += 1;
+    if(p->count <= g_budget)
+    {
+      uint64_t k = or_rand_int(&p->rand, g_n);         /* _rand.int(_num_ps) */
+      pony_sendi(ctx, (pony_actor_t*)g_ps[k], PING, 42);
+    }
+    g_x[p->idx] = p->rand.x; g_y[p->idx] = p->rand.y; g_count[p->idx] = p->count;
+  } else {
+    p->count += 1;
+    p->acc ^= payload;
+    uint64_t hop = payload & 0xFFFFFFFFULL;
+    if(hop < g_hops)
+    {
+      uint64_t k = or_mulhi(or_splitmix_mix(g_seed ^ payload), g_n);
+      pony_sendi(ctx, (pony_actor_t*)g_ps[k], PING,
+        (intptr_t)((payload & 0xFFFFFFFF00000000ULL) | (hop + 1)));
+    }
+    g_count[p->idx] = p->count; g_acc[p->idx] = p->acc;
+  }
+}
+
+static pony_type_t pinger_type = { .id = 2, .size = sizeof(pinger_t), .dispatch = pinger_dispatch };
+
+int main(int argc, char** argv)
+{
+  g_n = h_arg(argc, argv, "--pingers", 8);
+  uint64_t initial = h_arg(argc, argv, "--initial", 5);
+  g_budget = h_arg(argc, argv, "--budget", 100);
+  g_det = (int)h_arg(argc, argv, "--det", 0);
+  g_hops = h_arg(argc, argv, "--hops", 32);
+  g_seed = h_arg(argc, argv, "--seed", 5489);
+  int threads = (int)h_arg(argc, argv, "--threads", 1);
+  int noscale = (int)h_arg(argc, argv, "--noscale", 0);
+  const char* out = h_sarg(argc, argv, "--out", "");
+
+  g_ps = calloc(g_n, sizeof(pinger_t*));
+  g_x = calloc(g_n, 8); g_y = calloc(g_n, 8); g_count = calloc(g_n, 8); g_acc = calloc(g_n, 8);
+
+  pony_ctx_t* ctx = h_start(threads, noscale);
+
+  for(uint64_t i = 0; i < g_n; i++)
+  {
+    pinger_t* p = (pinger_t*)pony_create(ctx, &pinger_type);
+    p->idx = i;
+    p->count = 0;
+    p->acc = 0;
+    if(!g_det)
+    {
+      or_xoro_create(&p->rand, g_seed + i + 1, 0x9E3779B97F4A7C15ULL);
+      (void)or_rand_int(&p->rand, 100);
+      (void)or_rand_int(&p->rand, 100);
+      (void)or_rand_int(&p->rand, 100);
+      g_x[i] = p->rand.x; g_y[i] = p->rand.y;
+    }
+    g_ps[i] = p;
+  }
+  /* tell_all_to_go: for i in initial: for p in ps: p.ping(payload) */
+  for(uint64_t k = 0; k < initial; k++)
+    for(uint64_t i = 0; i < g_n; i++)
+    {
+      uint64_t payload = g_det ? ((i * initial + k) << 32) : 42;
+      pony_sendi(ctx, (pony_actor_t*)g_ps[i], PING, (intptr_t)payload);
+    }
+
+  double secs = h_run(ctx);
+
+  uint64_t total = 0;
+  for(uint64_t i = 0; i < g_n; i++) total += g_count[i];
+  h_report(g_det ? "ubench_det" : "ubench", threads, secs, total);
+  if(!g_det)
+  {
+    const uint64_t* f[3] = { g_x, g_y, g_count };
+    return h_dump(out, f, 3, g_n);
+  }
+  const uint64_t* f[2] = { g_count, g_acc };
+  return h_dump(out, f, 2, g_n);
+}
