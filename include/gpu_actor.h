@@ -84,6 +84,7 @@ typedef struct gpu_actor_counts_t
   uint64_t pending;     /* messages waiting in mailboxes now                 */
   uint64_t dropped;     /* messages lost to mailbox overflow (error)          */
   uint64_t remote;      /* messages that crossed ranks                       */
+  uint64_t active;      /* actor-steps that handled at least one message     */
   uint64_t delivered_by_type[GPU_ACTOR_MAX_TYPES];
 } gpu_actor_counts_t;
 

@@ -167,6 +167,7 @@ __global__ void __launch_bounds__(kBlock) k_drain()
   const unsigned long long snt = wave_sum(a.sent);
   const unsigned long long ap = wave_sum(a.applied);
   const unsigned long long so = wave_sum(a.seq >= kSeqLimit ? 1ull : 0ull);
+  const unsigned long long act = wave_sum(delivered ? 1ull : 0ull);
   // per-type delivered: uniform type per wave is the common case
   const int t0 = __builtin_amdgcn_readfirstlane(t);
   const bool uniform = __all(t == t0);
@@ -176,6 +177,7 @@ __global__ void __launch_bounds__(kBlock) k_drain()
     if(d + ap) atomicAdd(&c_eng.stats[ST_DELIVERED], d + ap);
     if(snt) atomicAdd(&c_eng.stats[ST_SENT], snt);
     if(so) atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], so);
+    if(act) atomicAdd(&c_eng.stats[ST_ACTIVE], act);
     if(uniform && d && t0 >= 0) atomicAdd(&c_eng.stats[ST_BY_TYPE + t0], d);
   }
   if(!uniform && delivered && t >= 0)
@@ -967,6 +969,7 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   out->pending = pend;
   out->dropped = st[ST_DROPPED] + st[ST_XCHG_OVERFLOW];
   out->remote = g.remote_total;
+  out->active = st[ST_ACTIVE];
   for(int t = 0; t < GPU_ACTOR_MAX_TYPES; ++t) out->delivered_by_type[t] = st[ST_BY_TYPE + t];
   return 0;
 }

@@ -27,7 +27,7 @@ constexpr uint32_t kSeqLimit = 1u << 24;      // per-sender sequence numbers per
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
-  ST_SEQ_OVERFLOW = 5, ST_XCHG_OVERFLOW = 6,
+  ST_SEQ_OVERFLOW = 5, ST_XCHG_OVERFLOW = 6, ST_ACTIVE = 7,
   ST_BY_TYPE = 16, ST_COUNT = 32
 };
 

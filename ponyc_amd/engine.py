@@ -63,6 +63,7 @@ class Counts(ctypes.Structure):
         ("pending", ctypes.c_uint64),
         ("dropped", ctypes.c_uint64),
         ("remote", ctypes.c_uint64),
+        ("active", ctypes.c_uint64),
         ("delivered_by_type", ctypes.c_uint64 * MAX_TYPES),
     ]
 
@@ -247,6 +248,7 @@ class Engine:
         return {
             "steps": c.steps, "delivered": c.delivered, "sent": c.sent,
             "pending": c.pending, "dropped": c.dropped, "remote": c.remote,
+            "active": c.active,
             "delivered_by_type": [c.delivered_by_type[i] for i in range(MAX_TYPES)],
         }
 
