@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--actors", type=int, default=1 << 20, help="pingers per GPU")
     p.add_argument("--initial", type=int, default=5)
-    p.add_argument("--mailbox-cap", type=int, default=64)
+    p.add_argument("--mailbox-cap", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-budget", type=int, default=40,
                    help="forward budget of the bounded CPU sample")

@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "engine.hip")
 DEPS = [SRC, os.path.join(HERE, "csrc", "engine_dev.h"), os.path.join(HERE, "csrc", "rng_dev.h"),
+        os.path.join(HERE, "csrc", "zone_dev.h"),
         os.path.join(ROOT, "include", "gpu_actor.h")]
 OUT = os.path.join(HERE, "libgpuactor.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

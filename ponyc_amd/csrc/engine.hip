@@ -1,17 +1,12 @@
-// engine.hip — the gpu_actor engine: superstep kernels for gfx950 and the C-ABI
-// declared in include/gpu_actor.h.
+// engine.hip — the gpu_actor engine for gfx950: kernels (zone_dev.h) and the
+// C-ABI declared in include/gpu_actor.h.
 //
-// One superstep = k_drain (every actor with visible mail drains up to `batch`
-// messages in canonical order and runs its handlers; sends go straight into
-// the receivers' HBM rings via one atomicAdd on the receiver's tail, or into a
-// per-peer exchange buffer when the receiver lives on another rank) followed by
-// k_snapshot (publishes the new tails as next step's visibility bound and
-// counts pending mail for the quiescence test). With n_ranks > 1 the exchange
-// buffers are swapped with RCCL between the two kernels and k_inject appends
-// the received records. This replaces ponyint_actor_run's pop loop
-// (actor.c:383-549), messageq push/pop (messageq.c:31-59,234-258), the run
-// queue/steal machinery (scheduler.c:752-1090) and per-message pool
-// allocation (pool.c:798-889).
+// One superstep = one k_step launch (one workgroup per 4096-actor zone; see
+// zone_dev.h). With n_ranks > 1, the records a step produced for actors on
+// other ranks are swapped with RCCL after it (counts all-to-all, then grouped
+// ncclSend/ncclRecv over xGMI) and k_xinject lands them before the next step.
+// The launch boundary is the BSP barrier; quiescence ("no pending mail on any
+// rank") replaces the CNF/ACK protocol (scheduler.c:303-480).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -23,248 +18,9 @@
 #include <vector>
 
 #include "engine_dev.h"
+#include "zone_dev.h"
 
 using namespace gpa;
-
-// ===========================================================================
-// Kernels
-// ===========================================================================
-
-// Drain one actor: `W` state words in registers for the whole drain.
-template <int HT>
-__device__ __forceinline__ void drain_actor(uint32_t L, const TypeDev& T, ActorCtx& a,
-  uint32_t& delivered, unsigned long long* s_agg)
-{
-  constexpr int W = HT_Words<HT>::W;
-  uint32_t head = c_eng.head[L];
-  const uint32_t end = c_eng.end[L];
-  if(head == end) return;
-  uint32_t sorted = c_eng.sorted[L];
-  const uint32_t mask = T.cap - 1;
-  Rec* ring = T.mb + (size_t)a.li * T.cap;
-  const uint32_t avail = end - head;
-  const uint32_t w = avail < T.batch ? avail : T.batch;
-
-  uint64_t s[W];
-#pragma unroll
-  for(int k = 0; k < W; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
-
-  uint32_t done = 0;
-  // 1. carried-over mail, already canonical
-  while(done < w && head + done != sorted)
-  {
-    const Rec r = ring[(head + done) & mask];
-    handle<HT>(T, a, s, r.sb & 0xFFu, r.arg, s_agg);
-    ++done;
-  }
-  // 2. the newest arrival group [sorted, end): deliver in (from, seq) order
-  if(sorted != end)
-  {
-    const uint32_t g = end - sorted;
-    const uint32_t q = w - done;
-    if(g == 1)
-    {
-      if(q >= 1)
-      {
-        const Rec r = ring[sorted & mask];
-        handle<HT>(T, a, s, r.sb & 0xFFu, r.arg, s_agg);
-        ++done;
-      }
-    }
-    else if(q >= g)
-    {
-      // whole group handled now: select in key order, no write-back
-      uint64_t last = 0;
-      for(uint32_t r = 0; r < g; ++r)
-      {
-        uint64_t best = ~0ull;
-        uint32_t bi = 0;
-        for(uint32_t j = 0; j < g; ++j)
-        {
-          const uint64_t k = rec_key(ring + ((sorted + j) & mask));
-          if((r == 0 || k > last) && k < best) { best = k; bi = j; }
-        }
-        const Rec rr = ring[(sorted + bi) & mask];
-        handle<HT>(T, a, s, rr.sb & 0xFFu, rr.arg, s_agg);
-        last = best;
-      }
-      done += g;
-    }
-    else
-    {
-      // part of the group carries over: canonicalise it in place first
-      for(uint32_t i = 1; i < g; ++i)
-      {
-        const Rec x = ring[(sorted + i) & mask];
-        const uint64_t kx = rec_key(&x);
-        uint32_t j = i;
-        while(j > 0)
-        {
-          const Rec y = ring[(sorted + j - 1) & mask];
-          if(rec_key(&y) <= kx) break;
-          ring[(sorted + j) & mask] = y;
-          --j;
-        }
-        ring[(sorted + j) & mask] = x;
-      }
-      for(uint32_t k = 0; k < q; ++k)
-      {
-        const Rec r = ring[(sorted + k) & mask];
-        handle<HT>(T, a, s, r.sb & 0xFFu, r.arg, s_agg);
-      }
-      done += q;
-    }
-    sorted = end;
-  }
-
-#pragma unroll
-  for(int k = 0; k < W; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
-  c_eng.head[L] = head + done;
-  c_eng.sorted[L] = sorted;
-  delivered += done;
-}
-
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
-{
-#pragma unroll
-  for(int off = 32; off > 0; off >>= 1)
-    v += __shfl_xor(v, off);
-  return v;
-}
-
-__global__ void __launch_bounds__(kBlock) k_drain()
-{
-  __shared__ unsigned long long s_agg[kWaves];
-  const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t delivered = 0;
-  ActorCtx a;
-  a.seq = 0; a.sent = 0; a.applied = 0; a.applied_type = -1;
-  int t = -1;
-  if(L < c_eng.n_local)
-  {
-    t = type_of_local(L);
-    if(t >= 0 && !c_types[t].reducible)
-    {
-      const TypeDev& T = c_types[t];
-      a.li = L - T.lfirst;
-      a.self = L * c_eng.nranks + c_eng.rank;
-      switch(T.ht)
-      {
-        case GPU_ACTOR_HT_RING:          drain_actor<GPU_ACTOR_HT_RING>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_PINGER:        drain_actor<GPU_ACTOR_HT_PINGER>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_PINGER_DET:    drain_actor<GPU_ACTOR_HT_PINGER_DET>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_FANIN_SENDER:  drain_actor<GPU_ACTOR_HT_FANIN_SENDER>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_GUPS_STREAMER: drain_actor<GPU_ACTOR_HT_GUPS_STREAMER>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_STORM:         drain_actor<GPU_ACTOR_HT_STORM>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_FIFO_SRC:      drain_actor<GPU_ACTOR_HT_FIFO_SRC>(L, T, a, delivered, s_agg); break;
-        case GPU_ACTOR_HT_FIFO_SINK:     drain_actor<GPU_ACTOR_HT_FIFO_SINK>(L, T, a, delivered, s_agg); break;
-        default: break;
-      }
-    }
-  }
-  // counters: one atomic per wave per counter (convergent here)
-  const unsigned long long d = wave_sum(delivered);
-  const unsigned long long snt = wave_sum(a.sent);
-  const unsigned long long ap = wave_sum(a.applied);
-  const unsigned long long so = wave_sum(a.seq >= kSeqLimit ? 1ull : 0ull);
-  const unsigned long long act = wave_sum(delivered ? 1ull : 0ull);
-  // per-type delivered: uniform type per wave is the common case
-  const int t0 = __builtin_amdgcn_readfirstlane(t);
-  const bool uniform = __all(t == t0);
-  const int lane = __lane_id();
-  if(lane == 0)
-  {
-    if(d + ap) atomicAdd(&c_eng.stats[ST_DELIVERED], d + ap);
-    if(snt) atomicAdd(&c_eng.stats[ST_SENT], snt);
-    if(so) atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], so);
-    if(act) atomicAdd(&c_eng.stats[ST_ACTIVE], act);
-    if(uniform && d && t0 >= 0) atomicAdd(&c_eng.stats[ST_BY_TYPE + t0], d);
-  }
-  if(!uniform && delivered && t >= 0)
-    atomicAdd(&c_eng.stats[ST_BY_TYPE + t], (unsigned long long)delivered);
-  // local applies to a reducible type (one target type per handler table)
-  if(a.applied && a.applied_type >= 0)
-    atomicAdd(&c_eng.stats[ST_BY_TYPE + a.applied_type], (unsigned long long)a.applied);
-}
-
-// Publish next step's visibility bound and count pending mail.
-__global__ void __launch_bounds__(kBlock) k_snapshot(uint32_t slot)
-{
-  __shared__ unsigned long long s_red[kWaves];
-  const uint32_t L = blockIdx.x * kBlock + threadIdx.x;
-  unsigned long long pend = 0;
-  if(L < c_eng.n_local)
-  {
-    const int t = type_of_local(L);
-    if(t >= 0 && !c_types[t].reducible)
-    {
-      const uint32_t tail = c_eng.tail[L];
-      const uint32_t head = c_eng.head[L];
-      c_eng.end[L] = tail;
-      c_eng.lim[L] = head + c_types[t].cap;
-      pend = tail - head;
-    }
-  }
-  pend = wave_sum(pend);
-  if(__lane_id() == 0) s_red[threadIdx.x >> 6] = pend;
-  __syncthreads();
-  if(threadIdx.x == 0)
-  {
-    unsigned long long tot = 0;
-    for(int w = 0; w < kWaves; ++w) tot += s_red[w];
-    if(tot) atomicAdd(&c_eng.pend[slot], tot);
-  }
-}
-
-// Host sends (pony_sendv from outside the runtime): hseq gives the canonical
-// order; records are appended exactly like device sends.
-__global__ void __launch_bounds__(kBlock) k_inject(const gpu_msg_t* msgs, uint64_t n,
-  uint64_t hseq_base)
-{
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if(i >= n) return;
-  const gpu_msg_t m = msgs[i];
-  const uint64_t hseq = hseq_base + i;
-  const uint32_t from = kHostFrom | (uint32_t)(hseq >> 24);
-  const uint32_t sb = (uint32_t)((hseq & 0xFFFFFFull) << 8) | (m.behaviour & 0xFFu);
-  if(c_eng.nranks > 1 && m.to % c_eng.nranks != c_eng.rank) return;   // not ours
-  const int t = type_of_global(m.to);
-  if(t < 0) return;
-  if(c_types[t].reducible)
-  {
-    reducible_apply_local(m.to, m.behaviour, m.arg);
-    atomicAdd(&c_eng.stats[ST_DELIVERED], 1ull);
-    atomicAdd(&c_eng.stats[ST_BY_TYPE + t], 1ull);
-    return;
-  }
-  ring_push(m.to, sb, from, m.arg);
-}
-
-// Records received from other ranks.
-__global__ void __launch_bounds__(kBlock) k_xinject(const XRec* in, uint64_t n)
-{
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if(i >= n) return;
-  const XRec x = in[i];
-  if(x.beh_only)
-    reducible_apply_local(x.to, x.sb, x.arg);
-  else
-    ring_push(x.to, x.sb, x.from, x.arg);
-}
-
-// Reducible deliveries that arrived from other ranks are counted at the
-// receiver so per-type counts stay exact under sharding.
-__global__ void k_xcount(const XRec* in, uint64_t n)
-{
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if(i >= n) return;
-  if(in[i].beh_only)
-  {
-    const int t = type_of_global(in[i].to);
-    atomicAdd(&c_eng.stats[ST_DELIVERED], 1ull);
-    if(t >= 0) atomicAdd(&c_eng.stats[ST_BY_TYPE + t], 1ull);
-  }
-}
 
 // pony_create's constructor run: initial state of a freshly created type.
 __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t)
@@ -276,8 +32,6 @@ __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t)
   const uint64_t i = (uint64_t)L * c_eng.nranks + c_eng.rank - T.first;   // index in type
   const size_t n = T.lcount;
   uint64_t* st = T.state;
-  c_eng.head[L] = 0; c_eng.sorted[L] = 0; c_eng.end[L] = 0; c_eng.tail[L] = 0;
-  c_eng.lim[L] = T.reducible ? 0u : T.cap;
   switch(T.ht)
   {
     case GPU_ACTOR_HT_RING: {
@@ -322,6 +76,16 @@ __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t)
   }
 }
 
+// Copy each zone's old buffer into its slot of a new layout (one block per zone).
+__global__ void __launch_bounds__(kBlock) k_zone_copy(const ZRec* src, const uint64_t* src_off,
+  const uint32_t* src_cap, ZRec* dst, const uint64_t* dst_off)
+{
+  const uint32_t z = blockIdx.x;
+  const ZRec* s = src + src_off[z];
+  ZRec* d = dst + dst_off[z];
+  for(uint32_t i = threadIdx.x; i < src_cap[z]; i += kBlock) d[i] = s[i];
+}
+
 // ===========================================================================
 // Host side
 // ===========================================================================
@@ -329,7 +93,8 @@ __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t)
 namespace {
 
 constexpr uint32_t kChunk = 16;          // steps between quiescence readbacks
-constexpr uint32_t kPendSlots = 4096;    // pend[] entries (chunk + run_fixed)
+constexpr uint32_t kPendSlots = 4096;    // pend[] entries
+constexpr uint32_t kPendPre = kPendSlots - 1;
 
 struct HostType {
   bool registered = false, created = false;
@@ -338,7 +103,6 @@ struct HostType {
   uint64_t first = 0, count = 0;
   uint32_t lfirst = 0, lcount = 0;
   uint64_t* d_state = nullptr;
-  Rec* d_mb = nullptr;
 };
 
 struct Engine {
@@ -350,9 +114,19 @@ struct Engine {
   HostType types[GPU_ACTOR_MAX_TYPES];
   uint32_t n_types = 0;                 // 1 + highest created type id
   uint64_t n_actors = 0;                // global ids handed out
-  uint32_t n_local = 0, local_cap = 0;
-  uint32_t *d_head = nullptr, *d_sorted = nullptr, *d_end = nullptr, *d_lim = nullptr,
-           *d_tail = nullptr;
+  uint32_t n_local = 0;
+  // zones
+  uint32_t n_zones = 0;
+  uint64_t zone_records = 0;
+  uint64_t* d_zoff = nullptr;
+  uint32_t* d_zcap = nullptr;
+  ZRec* d_land[2] = {nullptr, nullptr};
+  ZRec* d_carry[2] = {nullptr, nullptr};
+  uint32_t* d_land_n[2] = {nullptr, nullptr};
+  uint32_t* d_carry_n[2] = {nullptr, nullptr};
+  ZRec* d_S = nullptr;
+  ORec* d_O = nullptr;
+  uint32_t par = 0;                     // parity the next step reads
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_pend = nullptr;
   gpu_msg_t* h_msgs = nullptr; uint64_t h_msgs_cap = 0;
@@ -368,7 +142,7 @@ struct Engine {
   XRec* d_xout = nullptr;
   XRec* d_xin = nullptr;
   unsigned long long* d_xcount = nullptr;
-  unsigned long long* d_xrecv = nullptr;   // counts from each peer
+  unsigned long long* d_xrecv = nullptr;
   uint32_t xcap = 0;
   std::vector<unsigned long long> h_xcount, h_xrecv;
   uint64_t remote_total = 0;
@@ -406,7 +180,12 @@ inline uint64_t owned_below(uint64_t x)
   return x > rank() ? (x - rank() + R() - 1) / R() : 0;
 }
 
-inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+inline uint32_t blocks_for(uint64_t n, uint32_t bs = kBlock) { return (uint32_t)((n + bs - 1) / bs); }
+
+inline bool reducible_ht(uint32_t ht)
+{
+  return ht == GPU_ACTOR_HT_FANIN_ANALYZER || ht == GPU_ACTOR_HT_GUPS_UPDATER;
+}
 
 int upload_types()
 {
@@ -420,8 +199,8 @@ int upload_types()
     d.first = (uint32_t)h.first; d.count = (uint32_t)h.count;
     d.lfirst = h.lfirst; d.lcount = h.lcount;
     d.ht = h.ht; d.words = h.words; d.batch = h.batch; d.cap = h.cap;
-    d.reducible = (h.ht == GPU_ACTOR_HT_FANIN_ANALYZER || h.ht == GPU_ACTOR_HT_GUPS_UPDATER);
-    d.state = h.d_state; d.mb = h.d_mb;
+    d.reducible = reducible_ht(h.ht);
+    d.state = h.d_state;
     memcpy(d.params, h.params, sizeof(d.params));
   }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_types), td, sizeof(td), 0,
@@ -429,11 +208,95 @@ int upload_types()
   EngDev e;
   memset(&e, 0, sizeof(e));
   e.n_types = g.n_types; e.rank = rank(); e.nranks = R(); e.n_local = g.n_local;
-  e.head = g.d_head; e.sorted = g.d_sorted; e.end = g.d_end; e.lim = g.d_lim; e.tail = g.d_tail;
+  e.n_zones = g.n_zones; e.zoff = g.d_zoff; e.zcapz = g.d_zcap;
+  for(int p = 0; p < 2; ++p)
+  {
+    e.land[p] = g.d_land[p]; e.carry[p] = g.d_carry[p];
+    e.land_n[p] = g.d_land_n[p]; e.carry_n[p] = g.d_carry_n[p];
+  }
+  e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
+  return 0;
+}
+
+// Re-lay the zone buffers after actors were created: zone z holds
+// Σ_{serial actors in z} cap(type) records. Capacities only grow, so mail
+// already landed or carried is copied zone by zone into the new layout.
+int relayout_zones()
+{
+  const uint32_t nz = (uint32_t)((g.n_local + kZone - 1) / kZone);
+  if(nz > kMaxZones) return GPU_ACTOR_ERANGE;
+  std::vector<uint64_t> cap64(nz, 0);
+  for(const HostType& t : g.types)
+  {
+    if(!t.created || reducible_ht(t.ht)) continue;
+    for(uint64_t L = t.lfirst; L < (uint64_t)t.lfirst + t.lcount; )
+    {
+      const uint64_t z = L / kZone;
+      const uint64_t hi = std::min<uint64_t>((z + 1) * kZone, (uint64_t)t.lfirst + t.lcount);
+      cap64[z] += (hi - L) * t.cap;
+      L = hi;
+    }
+  }
+  std::vector<uint32_t> cap(nz);
+  std::vector<uint64_t> off(nz);
+  uint64_t total = 0;
+  for(uint32_t z = 0; z < nz; ++z)
+  {
+    if(cap64[z] > 0xFFFFFFF0ull) return GPU_ACTOR_ERANGE;
+    cap[z] = (uint32_t)cap64[z];
+    off[z] = total;
+    total += (cap[z] + 15u) & ~15u;          // keep every zone 256-B aligned
+  }
+  const size_t bytes = std::max<uint64_t>(total, 16) * sizeof(ZRec);
+  uint64_t* d_off = nullptr;
+  uint32_t* d_cap = nullptr;
+  HIPCK(hipMalloc(&d_off, std::max<size_t>(nz, 1) * sizeof(uint64_t)));
+  HIPCK(hipMalloc(&d_cap, std::max<size_t>(nz, 1) * sizeof(uint32_t)));
+  HIPCK(hipMemcpyAsync(d_off, off.data(), nz * sizeof(uint64_t), hipMemcpyHostToDevice, g.stream));
+  HIPCK(hipMemcpyAsync(d_cap, cap.data(), nz * sizeof(uint32_t), hipMemcpyHostToDevice, g.stream));
+  for(int p = 0; p < 2; ++p)
+  {
+    ZRec *land = nullptr, *carry = nullptr;
+    uint32_t *ln = nullptr, *cn = nullptr;
+    HIPCK(hipMalloc(&land, bytes));
+    HIPCK(hipMalloc(&carry, bytes));
+    HIPCK(hipMalloc(&ln, std::max<size_t>(nz, 1) * sizeof(uint32_t)));
+    HIPCK(hipMalloc(&cn, std::max<size_t>(nz, 1) * sizeof(uint32_t)));
+    HIPCK(hipMemsetAsync(ln, 0, std::max<size_t>(nz, 1) * sizeof(uint32_t), g.stream));
+    HIPCK(hipMemsetAsync(cn, 0, std::max<size_t>(nz, 1) * sizeof(uint32_t), g.stream));
+    if(g.n_zones)
+    {
+      hipLaunchKernelGGL(k_zone_copy, dim3(g.n_zones), dim3(kBlock), 0, g.stream,
+        (const ZRec*)g.d_land[p], g.d_zoff, g.d_zcap, land, (const uint64_t*)d_off);
+      hipLaunchKernelGGL(k_zone_copy, dim3(g.n_zones), dim3(kBlock), 0, g.stream,
+        (const ZRec*)g.d_carry[p], g.d_zoff, g.d_zcap, carry, (const uint64_t*)d_off);
+      HIPCK(hipGetLastError());
+      HIPCK(hipMemcpyAsync(ln, g.d_land_n[p], g.n_zones * sizeof(uint32_t),
+        hipMemcpyDeviceToDevice, g.stream));
+      HIPCK(hipMemcpyAsync(cn, g.d_carry_n[p], g.n_zones * sizeof(uint32_t),
+        hipMemcpyDeviceToDevice, g.stream));
+    }
+    HIPCK(hipStreamSynchronize(g.stream));
+    if(g.d_land[p]) HIPCK(hipFree(g.d_land[p]));
+    if(g.d_carry[p]) HIPCK(hipFree(g.d_carry[p]));
+    if(g.d_land_n[p]) HIPCK(hipFree(g.d_land_n[p]));
+    if(g.d_carry_n[p]) HIPCK(hipFree(g.d_carry_n[p]));
+    g.d_land[p] = land; g.d_carry[p] = carry; g.d_land_n[p] = ln; g.d_carry_n[p] = cn;
+  }
+  if(g.d_S) HIPCK(hipFree(g.d_S));
+  if(g.d_O) HIPCK(hipFree(g.d_O));
+  if(g.d_zoff) HIPCK(hipFree(g.d_zoff));
+  if(g.d_zcap) HIPCK(hipFree(g.d_zcap));
+  HIPCK(hipMalloc(&g.d_S, 2 * bytes));
+  HIPCK(hipMalloc(&g.d_O, std::max<uint64_t>(total, 16) * sizeof(ORec)));
+  g.d_zoff = d_off;
+  g.d_zcap = d_cap;
+  g.zone_records = total;
+  g.n_zones = nz;
   return 0;
 }
 
@@ -465,10 +328,10 @@ int check_sticky()
   return g.sticky;
 }
 
-// Cross-rank exchange of this step's remote records (RCCL over xGMI):
-// counts all-to-all, then grouped point-to-point record transfers, then
-// k_xinject appends them. Requires two small D2H reads of counts.
-int exchange()
+// Cross-rank exchange of the records a step produced for other ranks:
+// counts all-to-all, then grouped point-to-point transfers (RCCL over xGMI),
+// then k_xinject lands them for the next step. Two small D2H count reads.
+int exchange(uint32_t land_par)
 {
   const uint32_t n = R();
   HIPCK(hipMemcpyAsync(g.h_xcount.data(), g.d_xcount, n * sizeof(unsigned long long),
@@ -501,42 +364,46 @@ int exchange()
   if(total)
   {
     hipLaunchKernelGGL(k_xinject, dim3(blocks_for(total)), dim3(kBlock), 0, g.stream,
-      g.d_xin, total);
-    hipLaunchKernelGGL(k_xcount, dim3(blocks_for(total)), dim3(kBlock), 0, g.stream,
-      g.d_xin, total);
+      (const XRec*)g.d_xin, total, land_par);
     HIPCK(hipGetLastError());
   }
   HIPCK(hipMemsetAsync(g.d_xcount, 0, n * sizeof(unsigned long long), g.stream));
   return 0;
 }
 
+// One superstep: k_step on parity g.par (+ exchange), then flip parity.
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
-  const uint32_t nb = blocks_for(g.n_local);
-  if(nb == 0) return 0;
+  if(g.n_zones == 0) return 0;
   if(e0) HIPCK(hipEventRecord(e0, g.stream));
-  hipLaunchKernelGGL(k_drain, dim3(nb), dim3(kBlock), 0, g.stream);
+  hipLaunchKernelGGL(k_step, dim3(g.n_zones), dim3(kZoneThreads), 0, g.stream, g.par, slot);
   if(e1) HIPCK(hipEventRecord(e1, g.stream));
   HIPCK(hipGetLastError());
+  g.par ^= 1u;
   if(R() > 1)
   {
-    int rc = exchange();
+    int rc = exchange(g.par);
     if(rc) return rc;
   }
-  hipLaunchKernelGGL(k_snapshot, dim3(nb), dim3(kBlock), 0, g.stream, slot);
+  return 0;
+}
+
+int launch_pending(uint32_t slot)
+{
+  if(g.n_zones == 0) return 0;
+  hipLaunchKernelGGL(k_pending, dim3(blocks_for(g.n_zones)), dim3(kBlock), 0, g.stream,
+    g.par, slot);
   HIPCK(hipGetLastError());
   return 0;
 }
 
-// Sum of pending over all ranks for pend[slot] entries (host side, after sync).
+// Sum over ranks of pend[first .. first+n) (host side, after sync).
 int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out)
 {
   out.resize(n);
   if(R() > 1)
-  {
     NCCLCK(ncclAllReduce(g.d_pend + first, g.d_pend + first, n, ncclUint64, ncclSum, g.comm,
       g.stream));
-  }
   HIPCK(hipMemcpyAsync(out.data(), g.d_pend + first, n * sizeof(unsigned long long),
     hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
@@ -557,12 +424,18 @@ int ensure_events(size_t n)
 void free_all()
 {
   for(auto& t : g.types)
-  {
     if(t.d_state) (void)hipFree(t.d_state);
-    if(t.d_mb) (void)hipFree(t.d_mb);
+  for(int p = 0; p < 2; ++p)
+  {
+    if(g.d_land[p]) (void)hipFree(g.d_land[p]);
+    if(g.d_carry[p]) (void)hipFree(g.d_carry[p]);
+    if(g.d_land_n[p]) (void)hipFree(g.d_land_n[p]);
+    if(g.d_carry_n[p]) (void)hipFree(g.d_carry_n[p]);
   }
-  uint32_t* u32s[] = { g.d_head, g.d_sorted, g.d_end, g.d_lim, g.d_tail };
-  for(uint32_t* p : u32s) if(p) (void)hipFree(p);
+  if(g.d_S) (void)hipFree(g.d_S);
+  if(g.d_O) (void)hipFree(g.d_O);
+  if(g.d_zoff) (void)hipFree(g.d_zoff);
+  if(g.d_zcap) (void)hipFree(g.d_zcap);
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
   if(g.h_msgs) (void)hipHostFree(g.h_msgs);
@@ -574,6 +447,32 @@ void free_all()
   for(hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   if(g.comm) (void)ncclCommDestroy(g.comm);
   if(g.stream) (void)hipStreamDestroy(g.stream);
+}
+
+int sendv_locked(const gpu_msg_t* first, uint64_t n)
+{
+  if(n == 0) return 0;
+  if(!first) return GPU_ACTOR_EINVAL;
+  for(uint64_t i = 0; i < n; ++i)
+    if(first[i].to >= g.n_actors || first[i].behaviour > 0xF) return GPU_ACTOR_EINVAL;
+  if(g.host_seq + n >= (1ull << 40)) return GPU_ACTOR_ERANGE;
+  if(n > g.d_msgs_cap)
+  {
+    if(g.d_msgs) HIPCK(hipFree(g.d_msgs));
+    g.d_msgs = nullptr;
+    HIPCK(hipMalloc(&g.d_msgs, n * sizeof(gpu_msg_t)));
+    g.d_msgs_cap = n;
+  }
+  HIPCK(hipMemcpyAsync(g.d_msgs, first, n * sizeof(gpu_msg_t), hipMemcpyHostToDevice, g.stream));
+  if(g.n_zones)
+  {
+    hipLaunchKernelGGL(k_inject, dim3(blocks_for(n)), dim3(kBlock), 0, g.stream,
+      (const gpu_msg_t*)g.d_msgs, n, g.host_seq, g.par);
+    HIPCK(hipGetLastError());
+  }
+  g.host_seq += n;
+  HIPCK(hipStreamSynchronize(g.stream));    // the caller may reuse its buffer
+  return 0;
 }
 
 } // namespace
@@ -617,10 +516,9 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   if(!cfg) return GPU_ACTOR_EINVAL;
   g.cfg = *cfg;
   if(g.cfg.n_ranks == 0) g.cfg.n_ranks = 1;
-  if(g.cfg.rank >= g.cfg.n_ranks) return GPU_ACTOR_EINVAL;
+  if(g.cfg.rank >= g.cfg.n_ranks || g.cfg.n_ranks > kMaxRanks) return GPU_ACTOR_EINVAL;
   if(g.cfg.batch == 0) g.cfg.batch = 100;                 // PONY_SCHED_BATCH
-  if(g.cfg.mailbox_cap == 0) g.cfg.mailbox_cap = 64;
-  if(g.cfg.mailbox_cap & (g.cfg.mailbox_cap - 1)) return GPU_ACTOR_EINVAL;
+  if(g.cfg.mailbox_cap == 0) g.cfg.mailbox_cap = 16;
   if(g.cfg.max_actors == 0) g.cfg.max_actors = 1ull << 26;
   if(g.cfg.max_actors > 0xFF000000ull) return GPU_ACTOR_EINVAL;
 
@@ -632,13 +530,6 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipSetDevice(g.device));
   HIPCK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
 
-  g.local_cap = (uint32_t)((g.cfg.max_actors + R() - 1) / R());
-  const size_t lb = (size_t)g.local_cap * sizeof(uint32_t);
-  HIPCK(hipMalloc(&g.d_head, lb));
-  HIPCK(hipMalloc(&g.d_sorted, lb));
-  HIPCK(hipMalloc(&g.d_end, lb));
-  HIPCK(hipMalloc(&g.d_lim, lb));
-  HIPCK(hipMalloc(&g.d_tail, lb));
   HIPCK(hipMalloc(&g.d_stats, ST_COUNT * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats, 0, ST_COUNT * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
@@ -671,10 +562,15 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(g.stream) (void)hipStreamSynchronize(g.stream);
   free_all();
-  // reset to a pristine engine (mutex stays)
   for(auto& t : g.types) t = HostType();
-  g.init = false; g.n_types = 0; g.n_actors = 0; g.n_local = 0; g.local_cap = 0;
-  g.d_head = g.d_sorted = g.d_end = g.d_lim = g.d_tail = nullptr;
+  g.init = false; g.n_types = 0; g.n_actors = 0; g.n_local = 0;
+  g.n_zones = 0; g.zone_records = 0; g.d_zoff = nullptr; g.d_zcap = nullptr; g.par = 0;
+  for(int p = 0; p < 2; ++p)
+  {
+    g.d_land[p] = g.d_carry[p] = nullptr;
+    g.d_land_n[p] = g.d_carry_n[p] = nullptr;
+  }
+  g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
@@ -707,8 +603,8 @@ GPU_ACTOR_API int gpu_actor_type_config(uint32_t type_id, uint32_t batch, uint32
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(type_id >= GPU_ACTOR_MAX_TYPES || !g.types[type_id].registered) return GPU_ACTOR_EINVAL;
   HostType& t = g.types[type_id];
-  if(t.created && mailbox_cap && mailbox_cap != t.cap) return GPU_ACTOR_EINVAL;
   if(mailbox_cap & (mailbox_cap - 1)) return GPU_ACTOR_EINVAL;
+  if(t.created && mailbox_cap && mailbox_cap != t.cap) return GPU_ACTOR_EINVAL;
   if(batch) t.batch = batch;
   if(mailbox_cap) t.cap = mailbox_cap;
   return t.created ? upload_types() : 0;
@@ -737,22 +633,23 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
     const uint64_t size = t.params[0];
     if(size == 0 || (size & (size - 1)) || size > t.words) return GPU_ACTOR_EINVAL;
   }
+  const uint64_t lo = owned_below(g.n_actors), hi = owned_below(g.n_actors + count);
+  const uint32_t n_local = (uint32_t)hi;
+  if((n_local + kZone - 1) / kZone > kMaxZones) return GPU_ACTOR_ERANGE;
   t.first = g.n_actors;
   t.count = count;
-  const uint64_t lo = owned_below(t.first), hi = owned_below(t.first + count);
   t.lfirst = (uint32_t)lo;
   t.lcount = (uint32_t)(hi - lo);
   const size_t lc = std::max<size_t>(t.lcount, 1);
   HIPCK(hipMalloc(&t.d_state, (size_t)t.words * lc * sizeof(uint64_t)));
   HIPCK(hipMemsetAsync(t.d_state, 0, (size_t)t.words * lc * sizeof(uint64_t), g.stream));
-  const bool reducible = (t.ht == GPU_ACTOR_HT_FANIN_ANALYZER || t.ht == GPU_ACTOR_HT_GUPS_UPDATER);
-  if(!reducible)
-    HIPCK(hipMalloc(&t.d_mb, lc * t.cap * sizeof(Rec)));
   t.created = true;
   g.n_actors += count;
-  g.n_local = (uint32_t)owned_below(g.n_actors);
+  g.n_local = n_local;
   g.n_types = std::max(g.n_types, type_id + 1);
-  int rc = upload_types();
+  int rc = relayout_zones();
+  if(rc) return rc;
+  rc = upload_types();
   if(rc) return rc;
   if(t.lcount)
   {
@@ -781,29 +678,6 @@ GPU_ACTOR_API int gpu_actor_alloc_msgs(uint64_t n, gpu_msg_t** buf)
   return 0;
 }
 
-static int sendv_locked(const gpu_msg_t* first, uint64_t n)
-{
-  if(n == 0) return 0;
-  if(!first) return GPU_ACTOR_EINVAL;
-  for(uint64_t i = 0; i < n; ++i)
-    if(first[i].to >= g.n_actors || first[i].behaviour > 0xFF) return GPU_ACTOR_EINVAL;
-  if(g.host_seq + n >= (1ull << 48)) return GPU_ACTOR_ERANGE;
-  if(n > g.d_msgs_cap)
-  {
-    if(g.d_msgs) HIPCK(hipFree(g.d_msgs));
-    g.d_msgs = nullptr;
-    HIPCK(hipMalloc(&g.d_msgs, n * sizeof(gpu_msg_t)));
-    g.d_msgs_cap = n;
-  }
-  HIPCK(hipMemcpyAsync(g.d_msgs, first, n * sizeof(gpu_msg_t), hipMemcpyHostToDevice, g.stream));
-  hipLaunchKernelGGL(k_inject, dim3(blocks_for(n)), dim3(kBlock), 0, g.stream,
-    (const gpu_msg_t*)g.d_msgs, n, g.host_seq);
-  HIPCK(hipGetLastError());
-  g.host_seq += n;
-  HIPCK(hipStreamSynchronize(g.stream));    // caller may reuse its buffer
-  return 0;
-}
-
 GPU_ACTOR_API int gpu_actor_sendv(const gpu_msg_t* first, uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
@@ -815,9 +689,9 @@ GPU_ACTOR_API int gpu_actor_send(uint64_t to, uint32_t behaviour, uint64_t arg)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  if(to >= g.n_actors) return GPU_ACTOR_EINVAL;
   gpu_msg_t m;
   m.to = (uint32_t)to; m.behaviour = behaviour; m.arg = arg;
-  if(to >= g.n_actors) return GPU_ACTOR_EINVAL;
   return sendv_locked(&m, 1);
 }
 
@@ -825,34 +699,35 @@ GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
-  const uint32_t nb = blocks_for(g.n_local);
   uint64_t done = 0;
-  if(nb)
+  if(g.n_zones)
   {
-    // slot kPendSlots-1: pending before the first step
     HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-    hipLaunchKernelGGL(k_snapshot, dim3(nb), dim3(kBlock), 0, g.stream, kPendSlots - 1);
-    HIPCK(hipGetLastError());
+    int rc = launch_pending(kPendPre);
+    if(rc) return rc;
     std::vector<unsigned long long> pv;
-    int rc = pend_read(kPendSlots - 1, 1, pv);
+    rc = pend_read(kPendPre, 1, pv);
     if(rc) return rc;
     unsigned long long before = pv[0];
     while(before > 0 && (max_steps == 0 || done < max_steps))
     {
       uint32_t k = kChunk;
       if(max_steps) k = (uint32_t)std::min<uint64_t>(k, max_steps - done);
-      HIPCK(hipMemsetAsync(g.d_pend, 0, k * sizeof(unsigned long long), g.stream));
+      // pend[j] = pending at the start of step j (k_step), pend[k] = after the chunk
+      HIPCK(hipMemsetAsync(g.d_pend, 0, (k + 1) * sizeof(unsigned long long), g.stream));
       for(uint32_t j = 0; j < k; ++j)
       {
         rc = launch_step(j, nullptr, nullptr);
         if(rc) return rc;
       }
-      rc = pend_read(0, k, pv);
+      rc = launch_pending(k);
+      if(rc) return rc;
+      rc = pend_read(0, k + 1, pv);
       if(rc) return rc;
       for(uint32_t j = 0; j < k && before > 0; ++j)
       {
         ++done;
-        before = pv[j];
+        before = pv[j + 1];
       }
     }
   }
@@ -866,18 +741,16 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
-  const uint32_t nb = blocks_for(g.n_local);
-  if(nb == 0 || n == 0) return 0;
+  if(g.n_zones == 0 || n == 0) return 0;
   const uint64_t timed = std::min<uint64_t>(n, 2048);
   int rc = ensure_events(2 * timed);
   if(rc) return rc;
   HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-  hipLaunchKernelGGL(k_snapshot, dim3(nb), dim3(kBlock), 0, g.stream, kPendSlots - 1);
   for(uint64_t j = 0; j < n; ++j)
   {
     const bool tm = j >= n - timed;
     const uint64_t e = j - (n - timed);
-    rc = launch_step((uint32_t)(j % (kPendSlots - 1)), tm ? g.ev[2 * e] : nullptr,
+    rc = launch_step((uint32_t)(j % kPendPre), tm ? g.ev[2 * e] : nullptr,
       tm ? g.ev[2 * e + 1] : nullptr);
     if(rc) return rc;
   }
@@ -941,25 +814,21 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(!out) return GPU_ACTOR_EINVAL;
   unsigned long long st[ST_COUNT];
-  const uint32_t nb = blocks_for(g.n_local);
-  HIPCK(hipMemsetAsync(g.d_pend + kPendSlots - 1, 0, sizeof(unsigned long long), g.stream));
-  if(nb)
-  {
-    hipLaunchKernelGGL(k_snapshot, dim3(nb), dim3(kBlock), 0, g.stream, kPendSlots - 1);
-    HIPCK(hipGetLastError());
-  }
+  HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
+  int rc = launch_pending(kPendPre);
+  if(rc) return rc;
   const unsigned long long* src_stats = g.d_stats;
   if(R() > 1)
   {
-    // sum counters and pending over ranks into scratch (pend[0 .. ST_COUNT])
+    // sum counters and pending over ranks into scratch (pend[0 .. ST_COUNT))
     NCCLCK(ncclAllReduce(g.d_stats, g.d_pend, ST_COUNT, ncclUint64, ncclSum, g.comm, g.stream));
-    NCCLCK(ncclAllReduce(g.d_pend + kPendSlots - 1, g.d_pend + kPendSlots - 1, 1, ncclUint64,
+    NCCLCK(ncclAllReduce(g.d_pend + kPendPre, g.d_pend + kPendPre, 1, ncclUint64,
       ncclSum, g.comm, g.stream));
     src_stats = g.d_pend;
   }
   HIPCK(hipMemcpyAsync(st, src_stats, sizeof(st), hipMemcpyDeviceToHost, g.stream));
   unsigned long long pend = 0;
-  HIPCK(hipMemcpyAsync(&pend, g.d_pend + kPendSlots - 1, sizeof(pend), hipMemcpyDeviceToHost,
+  HIPCK(hipMemcpyAsync(&pend, g.d_pend + kPendPre, sizeof(pend), hipMemcpyDeviceToHost,
     g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   memset(out, 0, sizeof(*out));

@@ -1,17 +1,18 @@
-// engine_dev.h — device-side data layout and handler tables of the gpu_actor
-// engine. See DESIGN.md for the layout rationale.
+// engine_dev.h — device-side data layout, delivery primitives and handler
+// tables of the gpu_actor engine. See DESIGN.md for the rationale.
 //
-// HBM layout (per rank; actor id a lives on rank a % R at local slot a / R):
-//   per local slot (SoA, u32): head, sorted, end, lim, tail
-//     head   next slot to handle             (written by the owner's drain)
-//     sorted slots < sorted are in canonical order
-//     end    tail snapshot at the step start (messages in [head,end) are visible)
-//     lim    head at the step start + cap    (senders may fill slots < lim)
-//     tail   next free slot                  (senders: atomicAdd)
-//   per type: state[w][lcount] (u64, field-major) and a mailbox ring of
-//   cap x 16-B records per actor: {u32 seq<<8|beh, u32 from, u64 arg}. The first
-//   8 bytes read as one little-endian u64 are the canonical delivery key
-//   (from << 32 | seq << 8 | beh).
+// HBM layout (per rank; actor id a lives on rank a % R at local slot L = a / R):
+//   Local slots are cut into zones of kZone (4096) actors. Zone z owns
+//     land[p][z]   : landing buffer of step-p arrivals (unordered 16-B ZRecs),
+//                    filled by producers in chunks, one atomicAdd on
+//                    land_n[p][z] per (producer zone, destination zone);
+//     carry[p][z]  : mail handed over from the previous step because of the
+//                    batch limit, grouped by actor, in canonical order;
+//     S[z], O[z]   : per-zone scratch (sorted inbox, outbox) that the zone's
+//                    workgroup writes and reads back within one launch.
+//   Per type: state[w][lcount] (u64, field-major).
+// A ZRec is {u32 seq<<16 | beh<<12 | to_local, u32 from, u64 arg}; its
+// canonical delivery key is (from << 16 | seq).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,10 +21,18 @@
 
 namespace gpa {
 
-constexpr int      kBlock = 256;
+constexpr int      kBlock = 256;                 // helper kernels
 constexpr int      kWaves = kBlock / 64;
-constexpr uint32_t kHostFrom = 0xFF000000u;   // host senders: ids above every actor
-constexpr uint32_t kSeqLimit = 1u << 24;      // per-sender sequence numbers per step
+constexpr int      kZoneBits = 12;
+constexpr uint32_t kZone = 1u << kZoneBits;      // actors per zone
+constexpr uint32_t kZoneMask = kZone - 1;
+constexpr int      kZoneThreads = 1024;          // one workgroup per zone
+constexpr int      kZoneWaves = kZoneThreads / 64;
+constexpr uint32_t kMaxZones = 2048;             // LDS histogram bound (8M actors/rank)
+constexpr uint32_t kMaxRanks = 64;
+constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above every actor
+constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
+constexpr uint32_t kSeqApply = 0xFFFFu;          // outbox marker: reducible apply
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
@@ -31,19 +40,30 @@ enum Stat : int {
   ST_BY_TYPE = 16, ST_COUNT = 32
 };
 
-struct Rec {            // mailbox record, 16 B
-  uint32_t sb;          // seq << 8 | behaviour
-  uint32_t from;        // sender id (kHostFrom | hi bits for host sends)
+struct ZRec {            // landing / carry / sorted-inbox record, 16 B
+  uint32_t w0;           // seq << 16 | beh << 12 | to_local
+  uint32_t from;
   uint64_t arg;
 };
 
-struct XRec {           // cross-rank record, 24 B
+struct ORec {            // outbox record (zone scratch), 16 B
   uint32_t to;
-  uint32_t sb;
-  uint32_t from;
-  uint32_t beh_only;    // 1: reducible apply (seq unused)
+  uint32_t w;            // seq << 16 | beh << 12 | src_local
   uint64_t arg;
 };
+
+struct XRec {            // cross-rank record, 24 B
+  uint32_t to;
+  uint32_t w;            // seq << 16 | beh << 12 (seq == kSeqApply: reducible)
+  uint32_t from;
+  uint32_t pad;
+  uint64_t arg;
+};
+
+__device__ __forceinline__ uint64_t zkey(const ZRec& r)
+{
+  return ((uint64_t)r.from << 16) | (r.w0 >> 16);
+}
 
 struct TypeDev {
   uint32_t first, count;     // global id range
@@ -51,18 +71,25 @@ struct TypeDev {
   uint32_t ht, words, batch, cap;
   uint32_t reducible, pad;
   uint64_t* state;           // [words][lcount]
-  Rec*      mb;              // [lcount][cap]
   uint64_t  params[GPU_ACTOR_MAX_PARAMS];
 };
 
 struct EngDev {
   uint32_t n_types, rank, nranks, n_local;
-  uint32_t *head, *sorted, *end, *lim, *tail;
+  uint32_t n_zones, pad0;
+  const uint64_t* zoff;           // [n_zones] record offset of each zone's buffers
+  const uint32_t* zcapz;          // [n_zones] records a zone buffer holds
+  ZRec* land[2];                  // zone z: [zoff[z], zoff[z] + zcapz[z])
+  ZRec* carry[2];
+  uint32_t* land_n[2];            // [n_zones]
+  uint32_t* carry_n[2];
+  ZRec* S;                        // zone z: [2 zoff[z], 2 zoff[z] + 2 zcapz[z])
+  ORec* O;                        // zone z: [zoff[z], zoff[z] + zcapz[z])
   unsigned long long* stats;
   unsigned long long* pend;       // per-step pending counters
   XRec*  xout;                    // [nranks][xcap]
   unsigned long long* xcount;     // [nranks]
-  uint32_t xcap, pad;
+  uint32_t xcap, pad1;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -82,59 +109,42 @@ __device__ __forceinline__ int type_of_global(uint32_t id)
   return -1;
 }
 
-__device__ __forceinline__ uint64_t rec_key(const Rec* r)
+// records a zone's landing/carry/outbox buffer holds: the sum over its serial
+// actors of their type's mailbox capacity
+__device__ __forceinline__ uint32_t zone_capacity(uint32_t z)
 {
-  return *reinterpret_cast<const uint64_t*>(r);
+  return c_eng.zcapz[z];
+}
+
+// outbox bucket of a destination: its zone, or n_zones + peer rank if remote
+__device__ __forceinline__ uint32_t bucket_of(uint32_t to)
+{
+  const uint32_t R = c_eng.nranks;
+  if(R > 1)
+  {
+    const uint32_t owner = to % R;
+    if(owner != c_eng.rank) return c_eng.n_zones + owner;
+  }
+  return (to / R) >> kZoneBits;
 }
 
 // Per-lane bookkeeping while one actor drains.
 struct ActorCtx {
-  uint32_t self;       // global id
-  uint32_t li;         // index within its type (local)
-  uint32_t seq;        // emissions this step
+  uint32_t self;         // global id
+  uint32_t li;           // index within its type (local)
+  uint32_t src_local;    // slot within the zone
+  uint32_t seq;          // sends this step
   uint32_t sent;
-  uint32_t applied;    // reducible applies issued (delivered to applied_type)
+  uint32_t applied;      // local reducible applies issued
   int      applied_type;
+  ORec*     out;         // zone outbox (global scratch)
+  uint32_t  ocap;        // its capacity
+  uint32_t* s_nout;      // LDS outbox counter
+  uint32_t* s_hist;      // LDS histogram by bucket
+  unsigned long long* agg;   // this wave's LDS aggregation word
 };
 
-// ---- delivery ------------------------------------------------------------
-
-__device__ __forceinline__ void remote_append(uint32_t to, uint32_t sb, uint32_t from,
-  uint64_t arg, uint32_t beh_only)
-{
-  const uint32_t peer = to % c_eng.nranks;
-  const unsigned long long k = atomicAdd(&c_eng.xcount[peer], 1ull);
-  if(k >= c_eng.xcap)
-  {
-    atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], 1ull);
-    return;
-  }
-  XRec* x = c_eng.xout + (size_t)peer * c_eng.xcap + k;
-  x->to = to; x->sb = sb; x->from = from; x->beh_only = beh_only; x->arg = arg;
-}
-
-// Append one record to a serial actor's ring (local target).
-__device__ __forceinline__ void ring_push(uint32_t to, uint32_t sb, uint32_t from, uint64_t arg)
-{
-  const uint32_t L = to / c_eng.nranks;
-  const int t = type_of_global(to);
-  if(t < 0)
-  {
-    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
-    return;
-  }
-  const TypeDev& T = c_types[t];
-  const uint32_t slot = atomicAdd(&c_eng.tail[L], 1u);
-  if((int32_t)(slot - c_eng.lim[L]) >= 0)
-  {
-    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
-    return;
-  }
-  Rec* ring = T.mb + (size_t)(L - T.lfirst) * T.cap;
-  Rec r;
-  r.sb = sb; r.from = from; r.arg = arg;
-  *reinterpret_cast<uint4*>(ring + (slot & (T.cap - 1))) = *reinterpret_cast<const uint4*>(&r);
-}
+// ---- delivery --------------------------------------------------------------
 
 // Reducible behaviours: applied as device atomics at the owner.
 __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh, uint64_t arg)
@@ -162,36 +172,55 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
   (void)beh;
 }
 
-__device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t beh, uint64_t arg)
+// Park one record in the zone outbox and count it in its destination bucket.
+__device__ __forceinline__ void outbox_put(ActorCtx& a, uint32_t to, uint32_t w, uint64_t arg)
 {
-  const uint32_t sb = (a.seq << 8) | beh;
-  a.seq++;
-  a.sent++;
-  if(c_eng.nranks > 1 && to % c_eng.nranks != c_eng.rank)
+  const uint32_t idx = atomicAdd(a.s_nout, 1u);
+  if(idx >= a.ocap)
   {
-    remote_append(to, sb, a.self, arg, 0);
+    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
     return;
   }
-  ring_push(to, sb, a.self, arg);
+  ORec r;
+  r.to = to; r.w = w | a.src_local; r.arg = arg;
+  *reinterpret_cast<uint4*>(a.out + idx) = *reinterpret_cast<const uint4*>(&r);
+  atomicAdd(&a.s_hist[bucket_of(to)], 1u);
+}
+
+// A handler's send: stamped with its canonical (sender, seq) key now.
+__device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t beh, uint64_t arg)
+{
+  a.sent++;
+  if(a.seq >= kSeqMax)
+  {
+    atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
+    return;
+  }
+  outbox_put(a, to, (a.seq << 16) | (beh << 12), arg);
+  a.seq++;
+}
+
+__device__ __forceinline__ bool is_remote(uint32_t to)
+{
+  return c_eng.nranks > 1 && to % c_eng.nranks != c_eng.rank;
 }
 
 // fan-in Analyzer apply, aggregated per wavefront: lanes hitting the same
 // analyzer fold their count and XOR through LDS and one lane issues the two
 // global atomics (Guideline 12: one atomic per (wave, destination)).
-__device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t arg,
-  unsigned long long* s_agg)
+__device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t arg)
 {
   a.sent++;
-  const bool remote = c_eng.nranks > 1 && to % c_eng.nranks != c_eng.rank;
+  const bool remote = is_remote(to);
   if(remote)
-    remote_append(to, GPU_ACTOR_FANIN_MSG, a.self, arg, 1);   // counted by the owner
+    outbox_put(a, to, (kSeqApply << 16) | (GPU_ACTOR_FANIN_MSG << 12), arg);  // counted by owner
   else
   {
     a.applied++;
     if(a.applied_type < 0) a.applied_type = type_of_global(to);
   }
   const int lane = __lane_id();
-  const int wv = threadIdx.x >> 6;
+  unsigned long long* agg = a.agg;
   unsigned long long active = __ballot(!remote);
   while(active != 0ull)
   {
@@ -199,9 +228,9 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
     const uint32_t tl = __builtin_amdgcn_readlane(to, leader);
     const bool mine = !remote && to == tl;
     const unsigned long long peers = __ballot(mine);
-    if(lane == leader) s_agg[wv] = 0ull;
+    if(lane == leader) *agg = 0ull;
     __builtin_amdgcn_wave_barrier();
-    if(mine) atomicXor(&s_agg[wv], (unsigned long long)arg);
+    if(mine) atomicXor(agg, (unsigned long long)arg);
     __builtin_amdgcn_wave_barrier();
     if(lane == leader)
     {
@@ -213,7 +242,7 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
         atomicAdd(reinterpret_cast<unsigned long long*>(&T.state[li]),
           (unsigned long long)__popcll(peers));
         atomicXor(reinterpret_cast<unsigned long long*>(&T.state[(size_t)T.lcount + li]),
-          s_agg[wv]);
+          *agg);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -224,9 +253,9 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
 __device__ __forceinline__ void send_updater(ActorCtx& a, uint32_t to, uint64_t d)
 {
   a.sent++;
-  if(c_eng.nranks > 1 && to % c_eng.nranks != c_eng.rank)
+  if(is_remote(to))
   {
-    remote_append(to, GPU_ACTOR_GUPS_UPDATE, a.self, d, 1);   // counted by the owner
+    outbox_put(a, to, (kSeqApply << 16) | (GPU_ACTOR_GUPS_UPDATE << 12), d);  // counted by owner
     return;
   }
   a.applied++;
@@ -330,7 +359,7 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_FANIN_SENDER>(const TypeDev&
 {
   const uint64_t k = rand_int_unbiased(s[0], s[1], T.params[0]);
   const uint64_t i = a.self - T.first;
-  send_analyzer(a, (uint32_t)(T.params[1] + k), (i << 32) | s[3], s_agg);
+  send_analyzer(a, (uint32_t)(T.params[1] + k), (i << 32) | s[3]);
   s[3] += 1;
   if(s[2] > 0) s[2] -= 1;
   if(s[2] > 0)

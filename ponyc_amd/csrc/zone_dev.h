@@ -1,0 +1,502 @@
+// zone_dev.h — the superstep kernel (k_step) and the injection kernels.
+//
+// k_step runs one 1024-thread workgroup per zone of 4096 actors and replaces,
+// for those actors, ponyint_actor_run's pop loop (actor.c:383-549), the MPSC
+// push/pop (messageq.c:31-59,234-258) and the scheduler's run/steal loop
+// (scheduler.c:752-1090):
+//   1. count the zone's carried and newly landed records per actor (LDS
+//      atomics) and scan them into per-actor segments;
+//   2. place them into the zone's sorted-inbox scratch S (carry first, in
+//      canonical order; new arrivals after, in landing order);
+//   3. per actor: handle min(batch, n) messages — carried mail, then the new
+//      group in (from, seq) key order — with the actor's state in registers;
+//      sends are parked in the zone outbox O and counted per destination
+//      bucket (zone, or peer rank) in LDS; the unhandled tail is written to
+//      the zone's carry buffer for the next step, already canonical;
+//   4. reserve one contiguous chunk per destination bucket with ONE
+//      atomicAdd per (zone, bucket) and scatter the outbox into the
+//      destination zones' landing buffers (or the per-peer exchange buffer).
+// Workgroups never wait on each other: all inter-zone traffic goes through
+// the next launch (the step boundary is the BSP barrier).
+#pragma once
+#include "engine_dev.h"
+
+namespace gpa {
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+  for(int off = 32; off > 0; off >>= 1)
+    v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane)
+{
+#pragma unroll
+  for(int off = 1; off < 64; off <<= 1)
+  {
+    const uint32_t u = (uint32_t)__shfl_up((int)v, off);
+    if(lane >= (uint32_t)off) v += u;
+  }
+  return v;
+}
+
+// In-place exclusive scan of arr[kZone] (LDS) by a kZoneThreads workgroup;
+// returns the total. All threads must call it.
+__device__ uint32_t block_scan_zone(uint32_t* arr, uint32_t* s_tmp)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr uint32_t per = kZone / kZoneThreads;
+  uint32_t v[per];
+  uint32_t sum = 0;
+#pragma unroll
+  for(uint32_t k = 0; k < per; ++k) { v[k] = arr[tid * per + k]; sum += v[k]; }
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  if(lane == 63) s_tmp[wv] = incl;
+  __syncthreads();
+  if(wv == 0)
+  {
+    uint32_t x = lane < (uint32_t)kZoneWaves ? s_tmp[lane] : 0u;
+    x = wave_incl_scan(x, lane);
+    if(lane < (uint32_t)kZoneWaves) s_tmp[lane] = x;
+  }
+  __syncthreads();
+  uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
+#pragma unroll
+  for(uint32_t k = 0; k < per; ++k) { arr[tid * per + k] = run; run += v[k]; }
+  const uint32_t total = s_tmp[kZoneWaves - 1];
+  __syncthreads();
+  return total;
+}
+
+// Drain one actor from its segment seg[0..n) of the zone's sorted inbox:
+// seg[0..nc) is carried mail (canonical), seg[nc..n) the new arrival group.
+template <int HT>
+__device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, ZRec* seg,
+  uint32_t n, uint32_t nc, ZRec* cout, uint32_t cout_room)
+{
+  constexpr int NW = HT_Words<HT>::W;
+  const uint32_t w = n < T.batch ? n : T.batch;
+  uint64_t s[NW];
+#pragma unroll
+  for(int k = 0; k < NW; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
+  uint32_t done = 0;
+  while(done < w && done < nc)
+  {
+    const ZRec r = seg[done];
+    handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
+    ++done;
+  }
+  const uint32_t g = n - nc;
+  if(g > 0)
+  {
+    const uint32_t q = w - done;
+    ZRec* gs = seg + nc;
+    if(g == 1)
+    {
+      if(q >= 1)
+      {
+        const ZRec r = gs[0];
+        handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
+        ++done;
+      }
+    }
+    else if(q >= g)
+    {
+      // the whole group is handled now: select in key order (S is L1/L2-hot)
+      uint64_t last = 0;
+      for(uint32_t r = 0; r < g; ++r)
+      {
+        uint64_t best = ~0ull;
+        uint32_t bi = 0;
+        for(uint32_t j = 0; j < g; ++j)
+        {
+          const uint64_t k = zkey(gs[j]);
+          if((r == 0 || k > last) && k < best) { best = k; bi = j; }
+        }
+        const ZRec rr = gs[bi];
+        handle<HT>(T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg, nullptr);
+        last = best;
+      }
+      done += g;
+    }
+    else
+    {
+      // part of the group carries over: canonicalise it in place first
+      for(uint32_t i = 1; i < g; ++i)
+      {
+        const ZRec x = gs[i];
+        const uint64_t kx = zkey(x);
+        uint32_t j = i;
+        while(j > 0)
+        {
+          const ZRec y = gs[j - 1];
+          if(zkey(y) <= kx) break;
+          gs[j] = y;
+          --j;
+        }
+        gs[j] = x;
+      }
+      for(uint32_t k = 0; k < q; ++k)
+      {
+        const ZRec r = gs[k];
+        handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
+      }
+      done += q;
+    }
+  }
+#pragma unroll
+  for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
+  // the unhandled tail, canonical, becomes next step's carried mail
+  for(uint32_t k = done; k < n; ++k)
+  {
+    if(k - done < cout_room) cout[k - done] = seg[k];
+    else atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+  }
+  return done;
+}
+
+__global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pend_slot)
+{
+  __shared__ uint32_t s_cnt[kZone];     // records per actor this step
+  __shared__ uint32_t s_off[kZone];     // segment offset in S
+  __shared__ uint32_t s_ccnt[kZone];    // carried records per actor
+  __shared__ uint32_t s_aux[kZone];     // carry start -> landing cursor -> carry-out offset
+  __shared__ uint32_t s_hist[kMaxZones + kMaxRanks];
+  __shared__ uint32_t s_base[kMaxZones + kMaxRanks];
+  __shared__ uint32_t s_tmp[kZoneWaves + 1];
+  __shared__ uint32_t s_nout;
+  __shared__ unsigned long long s_agg[kZoneWaves];
+  __shared__ unsigned long long s_red[kZoneWaves][6];
+  __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
+
+  const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
+  const uint32_t nxt = cur ^ 1u;
+  const uint32_t L0 = z * kZone;
+  const uint32_t nact = min(kZone, c_eng.n_local - L0);
+  const uint32_t R = c_eng.nranks, me = c_eng.rank;
+  const uint32_t nz = c_eng.n_zones;
+  const uint32_t nb = nz + (R > 1 ? R : 0u);
+  const uint32_t cap = zone_capacity(z);
+
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
+  for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
+  if(tid == 0) s_nout = 0;
+  __syncthreads();
+
+  // ---- 1. count --------------------------------------------------------------
+  const uint32_t nc = min(c_eng.carry_n[cur][z], cap);
+  const uint32_t nl = min(c_eng.land_n[cur][z], cap);
+  const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
+  const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
+  for(uint32_t i = tid; i < nc; i += kZoneThreads)
+  {
+    const uint32_t a = C[i].w0 & kZoneMask;
+    atomicAdd(&s_cnt[a], 1u);
+    atomicAdd(&s_ccnt[a], 1u);
+  }
+  for(uint32_t i = tid; i < nl; i += kZoneThreads)
+    atomicAdd(&s_cnt[Ld[i].w0 & kZoneMask], 1u);
+  __syncthreads();
+  if(tid == 0)
+  {
+    if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
+    c_eng.carry_n[cur][z] = 0;
+    c_eng.land_n[cur][z] = 0;
+  }
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_off[i] = s_cnt[i]; s_aux[i] = s_ccnt[i]; }
+  __syncthreads();
+  (void)block_scan_zone(s_off, s_tmp);
+  (void)block_scan_zone(s_aux, s_tmp);
+
+  // ---- 2. place into the sorted inbox ---------------------------------------------
+  ZRec* Sz = c_eng.S + 2 * c_eng.zoff[z];
+  for(uint32_t i = tid; i < nc; i += kZoneThreads)
+  {
+    const ZRec r = C[i];
+    const uint32_t a = r.w0 & kZoneMask;
+    Sz[s_off[a] + (i - s_aux[a])] = r;
+  }
+  __syncthreads();
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
+  __syncthreads();
+  for(uint32_t i = tid; i < nl; i += kZoneThreads)
+  {
+    const ZRec r = Ld[i];
+    const uint32_t a = r.w0 & kZoneMask;
+    Sz[s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u)] = r;
+  }
+  __syncthreads();
+
+  // carry-out sizes (known before any handler runs) -> offsets
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+  {
+    uint32_t rem = 0;
+    const uint32_t n = s_cnt[i];
+    if(i < nact && n)
+    {
+      const int t = type_of_local(L0 + i);
+      if(t >= 0) rem = n > c_types[t].batch ? n - c_types[t].batch : 0u;
+    }
+    s_aux[i] = rem;
+  }
+  __syncthreads();
+  const uint32_t ncout = block_scan_zone(s_aux, s_tmp);
+  if(tid == 0)
+    c_eng.carry_n[nxt][z] = min(ncout, cap);
+
+  // ---- 3. run handlers -------------------------------------------------------------
+  ActorCtx a;
+  a.seq = 0; a.sent = 0; a.applied = 0; a.applied_type = -1;
+  a.out = c_eng.O + c_eng.zoff[z];
+  a.s_nout = &s_nout;
+  a.ocap = cap;
+  a.s_hist = s_hist;
+  a.agg = &s_agg[wv];
+  ZRec* Cout = c_eng.carry[nxt] + c_eng.zoff[z];
+  uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
+  for(uint32_t i = tid; i < nact; i += kZoneThreads)
+  {
+    const uint32_t n = s_cnt[i];
+    if(n == 0) continue;
+    const uint32_t L = L0 + i;
+    const int t = type_of_local(L);
+    if(t < 0 || c_types[t].reducible) continue;
+    const TypeDev& T = c_types[t];
+    a.li = L - T.lfirst;
+    a.self = L * R + me;
+    a.src_local = i;
+    a.seq = 0;
+    const uint32_t co = s_aux[i];
+    const uint32_t room = co < cap ? cap - co : 0u;
+    uint32_t d = 0;
+    switch(T.ht)
+    {
+#define ZCASE(HT) \
+      case HT: d = drain_zone<HT>(T, a, Sz + s_off[i], n, s_ccnt[i], Cout + co, room); break;
+      ZCASE(GPU_ACTOR_HT_RING)
+      ZCASE(GPU_ACTOR_HT_PINGER)
+      ZCASE(GPU_ACTOR_HT_PINGER_DET)
+      ZCASE(GPU_ACTOR_HT_FANIN_SENDER)
+      ZCASE(GPU_ACTOR_HT_GUPS_STREAMER)
+      ZCASE(GPU_ACTOR_HT_STORM)
+      ZCASE(GPU_ACTOR_HT_FIFO_SRC)
+      ZCASE(GPU_ACTOR_HT_FIFO_SINK)
+#undef ZCASE
+      default: break;
+    }
+    delivered += d;
+    active += d ? 1u : 0u;
+    if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
+  }
+  sent = a.sent;
+  applied = a.applied;
+  if(applied && a.applied_type >= 0)
+    atomicAdd(&s_bytype[a.applied_type], (unsigned long long)applied);
+  __syncthreads();
+  if(tid < GPU_ACTOR_MAX_TYPES && s_bytype[tid])
+    atomicAdd(&c_eng.stats[ST_BY_TYPE + tid], s_bytype[tid]);
+
+  // ---- 4. one chunk per destination bucket ----------------------------------------
+  for(uint32_t b = tid; b < nb; b += kZoneThreads)
+  {
+    const uint32_t h = s_hist[b];
+    if(h)
+    {
+      if(b < nz)
+        s_base[b] = atomicAdd(&c_eng.land_n[nxt][b], h);
+      else
+        s_base[b] = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
+    }
+    s_hist[b] = 0;
+  }
+  __syncthreads();
+  const uint32_t nout = min(s_nout, cap);
+  const ORec* Oz = c_eng.O + c_eng.zoff[z];
+  uint32_t dropped = 0, xover = 0;
+  for(uint32_t i = tid; i < nout; i += kZoneThreads)
+  {
+    const ORec o = Oz[i];
+    const uint32_t b = bucket_of(o.to);
+    const uint32_t pos = s_base[b] + atomicAdd(&s_hist[b], 1u);
+    const uint32_t from = (L0 + (o.w & kZoneMask)) * R + me;
+    if(b < nz)
+    {
+      if(pos < zone_capacity(b))
+      {
+        ZRec r;
+        r.w0 = (o.w & ~kZoneMask) | ((o.to / R) & kZoneMask);
+        r.from = from;
+        r.arg = o.arg;
+        *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos) =
+          *reinterpret_cast<const uint4*>(&r);
+      }
+      else
+        ++dropped;
+    }
+    else
+    {
+      if(pos < c_eng.xcap)
+      {
+        XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
+        x->to = o.to; x->w = o.w & ~kZoneMask; x->from = from; x->pad = 0; x->arg = o.arg;
+      }
+      else
+        ++xover;
+    }
+  }
+
+  // ---- counters: block reduction, one atomic per workgroup per counter ---------------
+  unsigned long long v[6] = { delivered + applied, sent, active, dropped, xover, 0 };
+#pragma unroll
+  for(int k = 0; k < 5; ++k)
+  {
+    v[k] = wave_sum(v[k]);
+    if(lane == 0) s_red[wv][k] = v[k];
+  }
+  __syncthreads();
+  if(tid < 5)
+  {
+    unsigned long long tot = 0;
+    for(int w = 0; w < kZoneWaves; ++w) tot += s_red[w][tid];
+    const int idx[5] = { ST_DELIVERED, ST_SENT, ST_ACTIVE, ST_DROPPED, ST_XCHG_OVERFLOW };
+    if(tot) atomicAdd(&c_eng.stats[idx[tid]], tot);
+  }
+}
+
+// Pending mail (carried + landed) for parity `cur`, summed into pend[slot].
+__global__ void __launch_bounds__(kBlock) k_pending(uint32_t cur, uint32_t slot)
+{
+  __shared__ unsigned long long s_red[kWaves];
+  const uint32_t z = blockIdx.x * kBlock + threadIdx.x;
+  unsigned long long p = 0;
+  if(z < c_eng.n_zones)
+  {
+    const uint32_t cap = zone_capacity(z);
+    p = min(c_eng.carry_n[cur][z], cap) + min(c_eng.land_n[cur][z], cap);
+  }
+  p = wave_sum(p);
+  if(__lane_id() == 0) s_red[threadIdx.x >> 6] = p;
+  __syncthreads();
+  if(threadIdx.x == 0)
+  {
+    unsigned long long tot = 0;
+    for(int w = 0; w < kWaves; ++w) tot += s_red[w];
+    if(tot) atomicAdd(&c_eng.pend[slot], tot);
+  }
+}
+
+// Block-aggregated landing of records addressed to this rank's serial actors:
+// one atomicAdd per (block, zone). Used for host sends and cross-rank records.
+__device__ __forceinline__ void land_block(bool valid, uint32_t to, uint32_t w_noto, uint32_t from,
+  uint64_t arg, uint32_t cur, uint32_t* s_hist, uint32_t* s_base)
+{
+  const uint32_t nz = c_eng.n_zones;
+  for(uint32_t b = threadIdx.x; b < nz; b += kBlock) s_hist[b] = 0;
+  __syncthreads();
+  uint32_t zt = 0;
+  if(valid)
+  {
+    zt = (to / c_eng.nranks) >> kZoneBits;
+    atomicAdd(&s_hist[zt], 1u);
+  }
+  __syncthreads();
+  for(uint32_t b = threadIdx.x; b < nz; b += kBlock)
+  {
+    if(s_hist[b]) s_base[b] = atomicAdd(&c_eng.land_n[cur][b], s_hist[b]);
+    s_hist[b] = 0;
+  }
+  __syncthreads();
+  if(valid)
+  {
+    const uint32_t pos = s_base[zt] + atomicAdd(&s_hist[zt], 1u);
+    if(pos < zone_capacity(zt))
+    {
+      ZRec r;
+      r.w0 = w_noto | ((to / c_eng.nranks) & kZoneMask);
+      r.from = from;
+      r.arg = arg;
+      *reinterpret_cast<uint4*>(c_eng.land[cur] + c_eng.zoff[zt] + pos) =
+        *reinterpret_cast<const uint4*>(&r);
+    }
+    else
+      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+  }
+}
+
+// Host sends (pony_sendv from outside the runtime): hseq gives the canonical
+// order; host senders rank above every actor id.
+__global__ void __launch_bounds__(kBlock) k_inject(const gpu_msg_t* msgs, uint64_t n,
+  uint64_t hseq_base, uint32_t cur)
+{
+  __shared__ uint32_t s_hist[kMaxZones];
+  __shared__ uint32_t s_base[kMaxZones];
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  bool valid = false;
+  uint32_t to = 0, w = 0, from = 0;
+  uint64_t arg = 0;
+  if(i < n)
+  {
+    const gpu_msg_t m = msgs[i];
+    const uint64_t hseq = hseq_base + i;
+    if(!is_remote(m.to))
+    {
+      const int t = type_of_global(m.to);
+      if(t >= 0 && c_types[t].reducible)
+      {
+        reducible_apply_local(m.to, m.behaviour, m.arg);
+        atomicAdd(&c_eng.stats[ST_DELIVERED], 1ull);
+        atomicAdd(&c_eng.stats[ST_BY_TYPE + t], 1ull);
+      }
+      else if(t >= 0)
+      {
+        valid = true;
+        to = m.to;
+        w = ((uint32_t)(hseq & 0xFFFFull) << 16) | ((m.behaviour & 0xFu) << 12);
+        from = kHostFrom | (uint32_t)(hseq >> 16);
+        arg = m.arg;
+      }
+    }
+  }
+  land_block(valid, to, w, from, arg, cur, s_hist, s_base);
+}
+
+// Records received from other ranks.
+__global__ void __launch_bounds__(kBlock) k_xinject(const XRec* in, uint64_t n, uint32_t cur)
+{
+  __shared__ uint32_t s_hist[kMaxZones];
+  __shared__ uint32_t s_base[kMaxZones];
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  bool valid = false;
+  uint32_t to = 0, w = 0, from = 0;
+  uint64_t arg = 0;
+  __shared__ unsigned long long s_app[GPU_ACTOR_MAX_TYPES];
+  if(threadIdx.x < GPU_ACTOR_MAX_TYPES) s_app[threadIdx.x] = 0;
+  __syncthreads();
+  if(i < n)
+  {
+    const XRec x = in[i];
+    if((x.w >> 16) == kSeqApply)
+    {
+      reducible_apply_local(x.to, (x.w >> 12) & 0xFu, x.arg);
+      const int t = type_of_global(x.to);
+      if(t >= 0) atomicAdd(&s_app[t], 1ull);
+    }
+    else
+    {
+      valid = true;
+      to = x.to; w = x.w; from = x.from; arg = x.arg;
+    }
+  }
+  land_block(valid, to, w, from, arg, cur, s_hist, s_base);
+  // land_block ends behind a barrier: s_app is complete
+  if(threadIdx.x < GPU_ACTOR_MAX_TYPES && s_app[threadIdx.x])
+  {
+    atomicAdd(&c_eng.stats[ST_DELIVERED], s_app[threadIdx.x]);
+    atomicAdd(&c_eng.stats[ST_BY_TYPE + threadIdx.x], s_app[threadIdx.x]);
+  }
+}
+
+} // namespace gpa
