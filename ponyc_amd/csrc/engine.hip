@@ -129,6 +129,7 @@ struct Engine {
   uint32_t par = 0;                     // parity the next step reads
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_pend = nullptr;
+  unsigned long long* d_dbg = nullptr;   // phase stamps of the diagnostic build
   gpu_msg_t* h_msgs = nullptr; uint64_t h_msgs_cap = 0;
   gpu_msg_t* d_msgs = nullptr; uint64_t d_msgs_cap = 0;
   uint64_t host_seq = 0;
@@ -217,6 +218,7 @@ int upload_types()
   e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
+  e.dbg = g.d_dbg;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   return 0;
@@ -376,7 +378,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
   if(e0) HIPCK(hipEventRecord(e0, g.stream));
-  hipLaunchKernelGGL(k_step, dim3(g.n_zones), dim3(kZoneThreads), 0, g.stream, g.par, slot);
+  const size_t dyn = 2 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
+  hipLaunchKernelGGL(k_step, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
   if(e1) HIPCK(hipEventRecord(e1, g.stream));
   HIPCK(hipGetLastError());
   g.par ^= 1u;
@@ -438,6 +441,7 @@ void free_all()
   if(g.d_zcap) (void)hipFree(g.d_zcap);
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
+  if(g.d_dbg) (void)hipFree(g.d_dbg);
   if(g.h_msgs) (void)hipHostFree(g.h_msgs);
   if(g.d_msgs) (void)hipFree(g.d_msgs);
   if(g.d_xout) (void)hipFree(g.d_xout);
@@ -533,6 +537,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_stats, ST_COUNT * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats, 0, ST_COUNT * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
+  HIPCK(hipMalloc(&g.d_dbg, kMaxZones * 8 * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * 8 * sizeof(unsigned long long), g.stream));
 
   if(R() > 1)
   {
@@ -571,7 +577,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
     g.d_land_n[p] = g.d_carry_n[p] = nullptr;
   }
   g.d_S = nullptr; g.d_O = nullptr;
-  g.d_stats = g.d_pend = nullptr;
+  g.d_stats = g.d_pend = g.d_dbg = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
@@ -852,5 +858,17 @@ GPU_ACTOR_API uint32_t gpu_actor_owner(uint64_t id)
 GPU_ACTOR_API void* gpu_actor_stream(void) { return (void*)g.stream; }
 
 GPU_ACTOR_API double gpu_actor_last_drain_ms(void) { return g.last_drain_ms; }
+
+// Diagnostic (not in the public header): phase stamps of the last k_step of
+// a -DGPA_STAMPS build, [n_zones][8] shader-clock values.
+GPU_ACTOR_API int gpu_actor_debug_stamps(uint64_t* out, uint64_t n)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init || !out) return GPU_ACTOR_ESTATE;
+  n = std::min<uint64_t>(n, (uint64_t)kMaxZones * 8);
+  HIPCK(hipMemcpyAsync(out, g.d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  return 0;
+}
 
 } // extern "C"

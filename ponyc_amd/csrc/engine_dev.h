@@ -23,12 +23,12 @@ namespace gpa {
 
 constexpr int      kBlock = 256;                 // helper kernels
 constexpr int      kWaves = kBlock / 64;
-constexpr int      kZoneBits = 12;
+constexpr int      kZoneBits = 11;               // to_local field holds up to 12 bits
 constexpr uint32_t kZone = 1u << kZoneBits;      // actors per zone
 constexpr uint32_t kZoneMask = kZone - 1;
-constexpr int      kZoneThreads = 1024;          // one workgroup per zone
+constexpr int      kZoneThreads = 512;           // one workgroup per zone
 constexpr int      kZoneWaves = kZoneThreads / 64;
-constexpr uint32_t kMaxZones = 2048;             // LDS histogram bound (8M actors/rank)
+constexpr uint32_t kMaxZones = 4096;             // histogram bound (8M actors/rank)
 constexpr uint32_t kMaxRanks = 64;
 constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above every actor
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
@@ -90,6 +90,7 @@ struct EngDev {
   XRec*  xout;                    // [nranks][xcap]
   unsigned long long* xcount;     // [nranks]
   uint32_t xcap, pad1;
+  unsigned long long* dbg;        // [n_zones][8] phase stamps (diagnostic build)
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];

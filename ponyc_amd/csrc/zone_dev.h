@@ -23,6 +23,20 @@
 
 namespace gpa {
 
+// Diagnostic build only (-DGPA_STAMPS): thread 0 of each zone stamps the
+// shader clock at phase boundaries into c_eng.dbg[zone * 8 + k]. The shipped
+// build compiles these away.
+#ifdef GPA_STAMPS
+#define GPA_STAMP(k)                                                         \
+  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
+#else
+#define GPA_STAMP(k) do {} while(0)
+#endif
+
+constexpr int kUnroll = 8;   // independent records in flight per thread in streaming loops
+constexpr int kScatterUnroll = 4;     // outbox records in flight per thread in the scatter
+constexpr uint32_t kIdxCap = 16384;   // LDS index budget per zone (records per step)
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
 #pragma unroll
@@ -70,10 +84,74 @@ __device__ uint32_t block_scan_zone(uint32_t* arr, uint32_t* s_tmp)
   return total;
 }
 
-// Drain one actor from its segment seg[0..n) of the zone's sorted inbox:
-// seg[0..nc) is carried mail (canonical), seg[nc..n) the new arrival group.
-template <int HT>
-__device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, ZRec* seg,
+__device__ __forceinline__ ZRec ld_rec(const ZRec* p)
+{
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  ZRec r;
+  r.w0 = v.x; r.from = v.y; r.arg = ((uint64_t)v.w << 32) | v.z;
+  return r;
+}
+
+// An actor's segment of the zone's records, in segment order: [0, nc) carried
+// mail (canonical), [nc, n) this step's arrival group (landing order).
+// AccIdx: an LDS index (u16) into carry ++ landing — the usual case.
+// AccS:   records materialised in the zone scratch S — zones whose record count
+//         exceeds the LDS index budget.
+struct AccIdx {
+  uint16_t* idx;
+  const ZRec* C;
+  const ZRec* Ld;
+  uint32_t nc_zone;
+  __device__ __forceinline__ ZRec rec(uint32_t j) const
+  {
+    const uint32_t i = idx[j];
+    return i < nc_zone ? ld_rec(C + i) : ld_rec(Ld + (i - nc_zone));
+  }
+  // insertion sort of [lo, lo + g) by canonical key
+  __device__ void sort(uint32_t lo, uint32_t g)
+  {
+    for(uint32_t i = 1; i < g; ++i)
+    {
+      const uint16_t x = idx[lo + i];
+      const uint64_t kx = zkey(rec(lo + i));
+      uint32_t j = i;
+      while(j > 0 && zkey(rec(lo + j - 1)) > kx)
+      {
+        idx[lo + j] = idx[lo + j - 1];
+        --j;
+      }
+      idx[lo + j] = x;
+    }
+  }
+};
+
+struct AccS {
+  ZRec* p;
+  __device__ __forceinline__ ZRec rec(uint32_t j) const { return ld_rec(p + j); }
+  __device__ void sort(uint32_t lo, uint32_t g)
+  {
+    for(uint32_t i = 1; i < g; ++i)
+    {
+      const ZRec x = p[lo + i];
+      const uint64_t kx = zkey(x);
+      uint32_t j = i;
+      while(j > 0)
+      {
+        const ZRec y = p[lo + j - 1];
+        if(zkey(y) <= kx) break;
+        p[lo + j] = y;
+        --j;
+      }
+      p[lo + j] = x;
+    }
+  }
+};
+
+// Drain one actor: handle min(batch, n) messages — carried mail, then the
+// arrival group in (from, seq) key order — and hand the canonical tail to the
+// next step's carry buffer.
+template <int HT, class Acc>
+__device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Acc acc,
   uint32_t n, uint32_t nc, ZRec* cout, uint32_t cout_room)
 {
   constexpr int NW = HT_Words<HT>::W;
@@ -84,27 +162,50 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, ZR
   uint32_t done = 0;
   while(done < w && done < nc)
   {
-    const ZRec r = seg[done];
+    const ZRec r = acc.rec(done);
     handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
     ++done;
   }
   const uint32_t g = n - nc;
+  bool sorted_tail = true;
   if(g > 0)
   {
     const uint32_t q = w - done;
-    ZRec* gs = seg + nc;
-    if(g == 1)
+    if(q >= g && g <= 8)
     {
-      if(q >= 1)
+      // small group handled whole: all records in registers, select by key
+      uint64_t k[8], v[8];
+      uint32_t bh[8];
+#pragma unroll
+      for(int j = 0; j < 8; ++j)
       {
-        const ZRec r = gs[0];
-        handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
-        ++done;
+        if((uint32_t)j < g)
+        {
+          const ZRec r = acc.rec(nc + j);
+          k[j] = zkey(r); v[j] = r.arg; bh[j] = (r.w0 >> 12) & 0xFu;
+        }
+        else
+        {
+          k[j] = ~0ull; v[j] = 0; bh[j] = 0;
+        }
       }
+      for(uint32_t r = 0; r < g; ++r)
+      {
+        uint64_t best = k[0], barg = v[0];
+        uint32_t bb = bh[0], bi = 0;
+#pragma unroll
+        for(int j = 1; j < 8; ++j)
+          if(k[j] < best) { best = k[j]; barg = v[j]; bb = bh[j]; bi = (uint32_t)j; }
+#pragma unroll
+        for(int j = 0; j < 8; ++j)
+          if((uint32_t)j == bi) k[j] = ~0ull;
+        handle<HT>(T, a, s, bb, barg, nullptr);
+      }
+      done += g;
     }
     else if(q >= g)
     {
-      // the whole group is handled now: select in key order (S is L1/L2-hot)
+      // large group handled whole: select in key order
       uint64_t last = 0;
       for(uint32_t r = 0; r < g; ++r)
       {
@@ -112,10 +213,10 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, ZR
         uint32_t bi = 0;
         for(uint32_t j = 0; j < g; ++j)
         {
-          const uint64_t k = zkey(gs[j]);
-          if((r == 0 || k > last) && k < best) { best = k; bi = j; }
+          const uint64_t kk = zkey(acc.rec(nc + j));
+          if((r == 0 || kk > last) && kk < best) { best = kk; bi = j; }
         }
-        const ZRec rr = gs[bi];
+        const ZRec rr = acc.rec(nc + bi);
         handle<HT>(T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg, nullptr);
         last = best;
       }
@@ -123,48 +224,44 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, ZR
     }
     else
     {
-      // part of the group carries over: canonicalise it in place first
-      for(uint32_t i = 1; i < g; ++i)
-      {
-        const ZRec x = gs[i];
-        const uint64_t kx = zkey(x);
-        uint32_t j = i;
-        while(j > 0)
-        {
-          const ZRec y = gs[j - 1];
-          if(zkey(y) <= kx) break;
-          gs[j] = y;
-          --j;
-        }
-        gs[j] = x;
-      }
+      // part of the group carries over: canonicalise it first
+      acc.sort(nc, g);
       for(uint32_t k = 0; k < q; ++k)
       {
-        const ZRec r = gs[k];
+        const ZRec r = acc.rec(nc + k);
         handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
       }
       done += q;
     }
   }
+  (void)sorted_tail;
 #pragma unroll
   for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
   // the unhandled tail, canonical, becomes next step's carried mail
   for(uint32_t k = done; k < n; ++k)
   {
-    if(k - done < cout_room) cout[k - done] = seg[k];
-    else atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    if(k - done < cout_room)
+    {
+      const ZRec r = acc.rec(k);
+      uint4 u;
+      u.x = r.w0; u.y = r.from; u.z = (uint32_t)r.arg; u.w = (uint32_t)(r.arg >> 32);
+      *reinterpret_cast<uint4*>(cout + (k - done)) = u;
+    }
+    else
+      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
   }
   return done;
 }
 
-__global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pend_slot)
+// 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
+__global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot)
 {
   __shared__ uint32_t s_cnt[kZone];     // records per actor this step
   __shared__ uint32_t s_off[kZone];     // segment offset in S
   __shared__ uint32_t s_ccnt[kZone];    // carried records per actor
   __shared__ uint32_t s_aux[kZone];     // carry start -> landing cursor -> carry-out offset
-  __shared__ uint32_t s_hist[kMaxZones + kMaxRanks];
-  __shared__ uint32_t s_base[kMaxZones + kMaxRanks];
+  __shared__ uint16_t s_idx[kIdxCap];   // per-actor segments: index into carry ++ landing
+  extern __shared__ uint32_t s_dyn[];       // [nb] histogram, [nb] chunk bases
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
   __shared__ uint32_t s_nout;
   __shared__ unsigned long long s_agg[kZoneWaves];
@@ -180,11 +277,14 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
   const uint32_t nz = c_eng.n_zones;
   const uint32_t nb = nz + (R > 1 ? R : 0u);
   const uint32_t cap = zone_capacity(z);
+  uint32_t* s_hist = s_dyn;
+  uint32_t* s_base = s_dyn + nb;
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
   for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
   if(tid == 0) s_nout = 0;
   __syncthreads();
+  GPA_STAMP(0);
 
   // ---- 1. count --------------------------------------------------------------
   const uint32_t nc = min(c_eng.carry_n[cur][z], cap);
@@ -197,9 +297,22 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
     atomicAdd(&s_cnt[a], 1u);
     atomicAdd(&s_ccnt[a], 1u);
   }
-  for(uint32_t i = tid; i < nl; i += kZoneThreads)
-    atomicAdd(&s_cnt[Ld[i].w0 & kZoneMask], 1u);
+  // 8 independent loads in flight per thread before their LDS atomics
+  for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
+  {
+    uint32_t w[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t i = base + u * kZoneThreads + tid;
+      w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      if(w[u] != 0xFFFFFFFFu) atomicAdd(&s_cnt[w[u] & kZoneMask], 1u);
+  }
   __syncthreads();
+  GPA_STAMP(1);
   if(tid == 0)
   {
     if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
@@ -210,25 +323,68 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
   __syncthreads();
   (void)block_scan_zone(s_off, s_tmp);
   (void)block_scan_zone(s_aux, s_tmp);
+  GPA_STAMP(2);
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
   ZRec* Sz = c_eng.S + 2 * c_eng.zoff[z];
+  const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
   for(uint32_t i = tid; i < nc; i += kZoneThreads)
   {
     const ZRec r = C[i];
     const uint32_t a = r.w0 & kZoneMask;
-    Sz[s_off[a] + (i - s_aux[a])] = r;
+    if(use_idx) s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
+    else Sz[s_off[a] + (i - s_aux[a])] = r;
   }
   __syncthreads();
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   __syncthreads();
-  for(uint32_t i = tid; i < nl; i += kZoneThreads)
+  if(use_idx)
   {
-    const ZRec r = Ld[i];
-    const uint32_t a = r.w0 & kZoneMask;
-    Sz[s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u)] = r;
+    // LDS index only: records stay in the landing buffer
+    for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
+    {
+      uint32_t w[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = base + u * kZoneThreads + tid;
+        w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        if(w[u] == 0xFFFFFFFFu) continue;
+        const uint32_t a = w[u] & kZoneMask;
+        s_idx[s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u)] =
+          (uint16_t)(nc + base + u * kZoneThreads + tid);
+      }
+    }
+  }
+  else
+  for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
+  {
+    uint4 r[kUnroll];
+    uint32_t pos[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t i = base + u * kZoneThreads + tid;
+      if(i < nl) r[u] = *reinterpret_cast<const uint4*>(Ld + i);
+      else r[u].x = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      if(r[u].x == 0xFFFFFFFFu) continue;
+      const uint32_t a = r[u].x & kZoneMask;
+      pos[u] = s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u);
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
   }
   __syncthreads();
+  GPA_STAMP(3);
 
   // carry-out sizes (known before any handler runs) -> offsets
   for(uint32_t i = tid; i < kZone; i += kZoneThreads)
@@ -274,8 +430,16 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
     uint32_t d = 0;
     switch(T.ht)
     {
-#define ZCASE(HT) \
-      case HT: d = drain_zone<HT>(T, a, Sz + s_off[i], n, s_ccnt[i], Cout + co, room); break;
+#define ZCASE(HT)                                                                     \
+      case HT:                                                                          \
+        if(use_idx)                                                                     \
+        {                                                                               \
+          AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                      \
+          d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], Cout + co, room);                 \
+        }                                                                               \
+        else                                                                            \
+          d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], Cout + co, room); \
+        break;
       ZCASE(GPU_ACTOR_HT_RING)
       ZCASE(GPU_ACTOR_HT_PINGER)
       ZCASE(GPU_ACTOR_HT_PINGER_DET)
@@ -296,6 +460,7 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
   if(applied && a.applied_type >= 0)
     atomicAdd(&s_bytype[a.applied_type], (unsigned long long)applied);
   __syncthreads();
+  GPA_STAMP(4);
   if(tid < GPU_ACTOR_MAX_TYPES && s_bytype[tid])
     atomicAdd(&c_eng.stats[ST_BY_TYPE + tid], s_bytype[tid]);
 
@@ -313,38 +478,59 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
     s_hist[b] = 0;
   }
   __syncthreads();
+  GPA_STAMP(5);
   const uint32_t nout = min(s_nout, cap);
   const ORec* Oz = c_eng.O + c_eng.zoff[z];
   uint32_t dropped = 0, xover = 0;
-  for(uint32_t i = tid; i < nout; i += kZoneThreads)
+  for(uint32_t base = 0; base < nout; base += kZoneThreads * kScatterUnroll)
   {
-    const ORec o = Oz[i];
-    const uint32_t b = bucket_of(o.to);
-    const uint32_t pos = s_base[b] + atomicAdd(&s_hist[b], 1u);
-    const uint32_t from = (L0 + (o.w & kZoneMask)) * R + me;
-    if(b < nz)
+    // ov = {to, w, arg lo, arg hi}
+    uint4 ov[kScatterUnroll];
+    uint32_t b[kScatterUnroll], pos[kScatterUnroll];
+#pragma unroll
+    for(int u = 0; u < kScatterUnroll; ++u)
     {
-      if(pos < zone_capacity(b))
-      {
-        ZRec r;
-        r.w0 = (o.w & ~kZoneMask) | ((o.to / R) & kZoneMask);
-        r.from = from;
-        r.arg = o.arg;
-        *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos) =
-          *reinterpret_cast<const uint4*>(&r);
-      }
-      else
-        ++dropped;
+      const uint32_t i = base + u * kZoneThreads + tid;
+      if(i < nout) ov[u] = *reinterpret_cast<const uint4*>(Oz + i);
+      else ov[u].y = 0xFFFFFFFFu;
     }
-    else
+#pragma unroll
+    for(int u = 0; u < kScatterUnroll; ++u)
     {
-      if(pos < c_eng.xcap)
+      if(ov[u].y == 0xFFFFFFFFu) continue;
+      b[u] = bucket_of(ov[u].x);
+      pos[u] = s_base[b[u]] + atomicAdd(&s_hist[b[u]], 1u);
+    }
+#pragma unroll
+    for(int u = 0; u < kScatterUnroll; ++u)
+    {
+      if(ov[u].y == 0xFFFFFFFFu) continue;
+      const uint32_t from = (L0 + (ov[u].y & kZoneMask)) * R + me;
+      if(b[u] < nz)
       {
-        XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
-        x->to = o.to; x->w = o.w & ~kZoneMask; x->from = from; x->pad = 0; x->arg = o.arg;
+        if(pos[u] < zone_capacity(b[u]))
+        {
+          uint4 v;
+          v.x = (ov[u].y & ~kZoneMask) | ((ov[u].x / R) & kZoneMask);
+          v.y = from;
+          v.z = ov[u].z;
+          v.w = ov[u].w;
+          *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b[u]] + pos[u]) = v;
+        }
+        else
+          ++dropped;
       }
       else
-        ++xover;
+      {
+        if(pos[u] < c_eng.xcap)
+        {
+          XRec* x = c_eng.xout + (size_t)(b[u] - nz) * c_eng.xcap + pos[u];
+          x->to = ov[u].x; x->w = ov[u].y & ~kZoneMask; x->from = from; x->pad = 0;
+          x->arg = ((uint64_t)ov[u].w << 32) | ov[u].z;
+        }
+        else
+          ++xover;
+      }
     }
   }
 
@@ -357,12 +543,14 @@ __global__ void __launch_bounds__(kZoneThreads) k_step(uint32_t cur, uint32_t pe
     if(lane == 0) s_red[wv][k] = v[k];
   }
   __syncthreads();
+  GPA_STAMP(6);
   if(tid < 5)
   {
     unsigned long long tot = 0;
     for(int w = 0; w < kZoneWaves; ++w) tot += s_red[w][tid];
-    const int idx[5] = { ST_DELIVERED, ST_SENT, ST_ACTIVE, ST_DROPPED, ST_XCHG_OVERFLOW };
-    if(tot) atomicAdd(&c_eng.stats[idx[tid]], tot);
+    const int idx = tid == 0 ? ST_DELIVERED : tid == 1 ? ST_SENT : tid == 2 ? ST_ACTIVE
+                  : tid == 3 ? ST_DROPPED : ST_XCHG_OVERFLOW;
+    if(tot) atomicAdd(&c_eng.stats[idx], tot);
   }
 }
 

@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpuactor.so")
+# PONYC_AMD_LIB selects another in-tree build (e.g. the stamps diagnostic)
+LIB_PATH = os.environ.get("PONYC_AMD_LIB", os.path.join(_HERE, "libgpuactor.so"))
 
 MSG_DTYPE = np.dtype([("to", "<u4"), ("behaviour", "<u4"), ("arg", "<u8")])
 MAX_TYPES = 16
