@@ -13,9 +13,10 @@ the K timed steps.
 
 Also reported:
   roofline     — the drain kernel's algorithmic HBM bytes per launch
-                 (32 B per message: 16-B record written by the sender and read
-                 by the receiver; 2*S + 16 B per active actor: state read+write
-                 and the mailbox header) / its HIP-event-timed average duration;
+                 (32 B per message: 16-B record written by the sender's zone and
+                 read by the receiver's zone; 2*S per active actor: state read +
+                 write, S = 24 B for a pinger) / its HIP-event-timed average
+                 duration (k_step, on the engine's stream);
   cpu_baseline — the reference runtime (oracle/_ref/libponyrt.so, built from
                  KittyMac/ponyc src/libponyrt) running the same pinger graph via
                  oracle/_ref/harness_ubench on this host's cores (rank 0, N=1).
@@ -36,7 +37,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PINGER_STATE_BYTES = 24        # rng x, y + count
-MAILBOX_HDR_BYTES = 16         # head, sorted, end, lim (u32) read/written per active actor
 REC_BYTES = 16
 
 
@@ -132,9 +132,25 @@ def main():
     if world > 1:
         comm = bcast_bytes(pg, rank, Engine.comm_id() if rank == 0 else None)
     n_total = args.actors * world
-    eng = Engine(device=local, n_ranks=world, rank=rank, mailbox_cap=args.mailbox_cap,
-                 max_actors=n_total + 1024, comm_id=comm,
-                 max_exchange=max(1 << 20, 2 * args.actors * args.initial // max(world, 1)))
+    kw = dict(device=local, n_ranks=world, rank=rank, mailbox_cap=args.mailbox_cap,
+              max_actors=n_total + 1024,
+              max_exchange=max(1 << 20, 2 * args.actors * args.initial // max(world, 1)))
+    exchange = "none" if world == 1 else "rccl"
+    try:
+        eng = Engine(comm_id=comm, **kw)
+        ok = 1.0
+    except Exception as exc:        # RCCL unusable: say so, measure the host exchange
+        if world == 1:
+            raise
+        print(f"rank {rank}: RCCL exchange unavailable ({exc}); using the host transport",
+              file=sys.stderr)
+        ok = 0.0
+    if world > 1 and allmax(pg, 1.0 - ok) > 0:
+        if ok:
+            eng.shutdown()
+        from ponyc_amd.dist import GlooTransport
+        eng = Engine(transport=GlooTransport(), **kw)
+        exchange = "host-staged (gloo)"
     # steady state: budget never reached
     budget = (1 << 62)
     ty = 0
@@ -177,11 +193,10 @@ def main():
     # roofline of the drain kernel on this rank (per launch)
     msgs_per_step = delivered / args.steps / world
     active_per_step = active / args.steps / world
-    alg_bytes = msgs_per_step * 2 * REC_BYTES + active_per_step * (2 * PINGER_STATE_BYTES
-                                                                     + MAILBOX_HDR_BYTES)
+    alg_bytes = msgs_per_step * 2 * REC_BYTES + active_per_step * 2 * PINGER_STATE_BYTES
     achieved = alg_bytes / (drain_ms * 1e-3) / 1e9 if drain_ms > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_drain_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_step_r01.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -213,6 +228,7 @@ def main():
                 "actors_per_gpu": args.actors, "actors_total": n_total,
                 "initial_pings": args.initial, "mailbox_cap": args.mailbox_cap, "batch": 100,
                 "parallelism": f"actor hash partition x{world} (id % {world})",
+                "exchange": exchange,
             },
             "msgs_per_step": round(delivered / args.steps, 1),
             "dropped": dropped,
@@ -220,7 +236,7 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_drain", "drain_ms": round(drain_ms, 4),
+                "kernel": "k_step", "kernel_ms": round(drain_ms, 4),
                 "alg_bytes_per_launch": round(alg_bytes, 1),
             },
             "cpu_baseline": cpu,

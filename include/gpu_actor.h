@@ -94,6 +94,19 @@ GPU_ACTOR_API int gpu_actor_shutdown(void);
 /* 128-byte communicator id to broadcast from rank 0 before gpu_actor_init. */
 GPU_ACTOR_API int gpu_actor_comm_id(void* out128);
 
+/* Host transport for n_ranks > 1 when no RCCL communicator is given (comm_id
+ * NULL): the per-step exchange and the cross-rank sums are routed through these
+ * host callbacks (e.g. gloo), with records staged through pinned host memory.
+ * alltoallv: send_bytes[p] bytes at offset Σ_{q<p} send_bytes[q] of `send` go
+ * to rank p; recv_bytes[p] bytes from rank p land likewise in `recv`. Returns
+ * 0 on success. allreduce: in-place sum of n u64 over ranks. Set before
+ * gpu_actor_init; NULL restores RCCL. */
+typedef int (*gpu_actor_alltoallv_fn)(void* ctx, const void* send, const uint64_t* send_bytes,
+  void* recv, const uint64_t* recv_bytes);
+typedef int (*gpu_actor_allreduce_fn)(void* ctx, uint64_t* buf, uint64_t n);
+GPU_ACTOR_API int gpu_actor_set_transport(gpu_actor_alltoallv_fn alltoallv,
+  gpu_actor_allreduce_fn allreduce, void* ctx);
+
 /* ---- types (pony_type_t, pony.h:171-195) -------------------------------- */
 /* Register actor type `type_id` (< GPU_ACTOR_MAX_TYPES) with `state_words`
  * 64-bit words of POD state, dispatching to handler table `handler_table`

@@ -147,6 +147,12 @@ struct Engine {
   uint32_t xcap = 0;
   std::vector<unsigned long long> h_xcount, h_xrecv;
   uint64_t remote_total = 0;
+  // host transport (gpu_actor_set_transport)
+  gpu_actor_alltoallv_fn xp_a2a = nullptr;
+  gpu_actor_allreduce_fn xp_ar = nullptr;
+  void* xp_ctx = nullptr;
+  XRec* h_xout = nullptr;
+  XRec* h_xin = nullptr;
 };
 
 Engine g;
@@ -333,34 +339,75 @@ int check_sticky()
 // Cross-rank exchange of the records a step produced for other ranks:
 // counts all-to-all, then grouped point-to-point transfers (RCCL over xGMI),
 // then k_xinject lands them for the next step. Two small D2H count reads.
-int exchange(uint32_t land_par)
+// Host transport: the same exchange with records staged through pinned host
+// memory and the collectives done by the registered callbacks (gloo etc.).
+int exchange_host(uint64_t& total)
 {
   const uint32_t n = R();
   HIPCK(hipMemcpyAsync(g.h_xcount.data(), g.d_xcount, n * sizeof(unsigned long long),
     hipMemcpyDeviceToHost, g.stream));
-  NCCLCK(ncclAllToAll(g.d_xcount, g.d_xrecv, 1, ncclUint64, g.comm, g.stream));
-  HIPCK(hipMemcpyAsync(g.h_xrecv.data(), g.d_xrecv, n * sizeof(unsigned long long),
-    hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
+  std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n);
+  for(uint32_t p = 0; p < n; ++p)
+    sc[p] = p == rank() ? 0 : std::min<unsigned long long>(g.h_xcount[p], g.xcap);
+  std::vector<uint64_t> rc(n, 0);
+  if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rc.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
+  uint64_t soff = 0, roff = 0;
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    rc[p] = std::min<uint64_t>(rc[p], g.xcap);
+    if(sc[p])
+      HIPCK(hipMemcpyAsync(g.h_xout + soff, g.d_xout + (size_t)p * g.xcap, sc[p] * sizeof(XRec),
+        hipMemcpyDeviceToHost, g.stream));
+    soff += sc[p];
+    roff += rc[p];
+    sb[p] = sc[p] * sizeof(XRec);
+    rb[p] = rc[p] * sizeof(XRec);
+  }
+  HIPCK(hipStreamSynchronize(g.stream));
+  if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
+  if(roff)
+    HIPCK(hipMemcpyAsync(g.d_xin, g.h_xin, roff * sizeof(XRec), hipMemcpyHostToDevice, g.stream));
+  total = roff;
+  return 0;
+}
+
+int exchange(uint32_t land_par)
+{
+  const uint32_t n = R();
   uint64_t off = 0;
-  std::vector<uint64_t> roff(n);
-  for(uint32_t p = 0; p < n; ++p)
+  if(g.xp_a2a)
   {
-    roff[p] = off;
-    off += std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
+    int rc = exchange_host(off);
+    if(rc) return rc;
   }
-  NCCLCK(ncclGroupStart());
-  for(uint32_t p = 0; p < n; ++p)
+  else
   {
-    if(p == rank()) continue;
-    const uint64_t sc = std::min<unsigned long long>(g.h_xcount[p], g.xcap);
-    const uint64_t rc = std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
-    if(sc) NCCLCK(ncclSend(g.d_xout + (size_t)p * g.xcap, sc * sizeof(XRec), ncclUint8, p,
-      g.comm, g.stream));
-    if(rc) NCCLCK(ncclRecv(g.d_xin + roff[p], rc * sizeof(XRec), ncclUint8, p, g.comm,
-      g.stream));
+    HIPCK(hipMemcpyAsync(g.h_xcount.data(), g.d_xcount, n * sizeof(unsigned long long),
+      hipMemcpyDeviceToHost, g.stream));
+    NCCLCK(ncclAllToAll(g.d_xcount, g.d_xrecv, 1, ncclUint64, g.comm, g.stream));
+    HIPCK(hipMemcpyAsync(g.h_xrecv.data(), g.d_xrecv, n * sizeof(unsigned long long),
+      hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    std::vector<uint64_t> roff(n);
+    for(uint32_t p = 0; p < n; ++p)
+    {
+      roff[p] = off;
+      off += std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
+    }
+    NCCLCK(ncclGroupStart());
+    for(uint32_t p = 0; p < n; ++p)
+    {
+      if(p == rank()) continue;
+      const uint64_t sc = std::min<unsigned long long>(g.h_xcount[p], g.xcap);
+      const uint64_t rc = std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
+      if(sc) NCCLCK(ncclSend(g.d_xout + (size_t)p * g.xcap, sc * sizeof(XRec), ncclUint8, p,
+        g.comm, g.stream));
+      if(rc) NCCLCK(ncclRecv(g.d_xin + roff[p], rc * sizeof(XRec), ncclUint8, p, g.comm,
+        g.stream));
+    }
+    NCCLCK(ncclGroupEnd());
   }
-  NCCLCK(ncclGroupEnd());
   const uint64_t total = off;
   g.remote_total += total;
   if(total)
@@ -404,12 +451,15 @@ int launch_pending(uint32_t slot)
 int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out)
 {
   out.resize(n);
-  if(R() > 1)
+  if(R() > 1 && !g.xp_ar)
     NCCLCK(ncclAllReduce(g.d_pend + first, g.d_pend + first, n, ncclUint64, ncclSum, g.comm,
       g.stream));
   HIPCK(hipMemcpyAsync(out.data(), g.d_pend + first, n * sizeof(unsigned long long),
     hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
+  if(R() > 1 && g.xp_ar &&
+    g.xp_ar(g.xp_ctx, reinterpret_cast<uint64_t*>(out.data()), n) != 0)
+    return GPU_ACTOR_ECOMM;
   return 0;
 }
 
@@ -448,6 +498,8 @@ void free_all()
   if(g.d_xin) (void)hipFree(g.d_xin);
   if(g.d_xcount) (void)hipFree(g.d_xcount);
   if(g.d_xrecv) (void)hipFree(g.d_xrecv);
+  if(g.h_xout) (void)hipHostFree(g.h_xout);
+  if(g.h_xin) (void)hipHostFree(g.h_xin);
   for(hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   if(g.comm) (void)ncclCommDestroy(g.comm);
   if(g.stream) (void)hipStreamDestroy(g.stream);
@@ -542,11 +594,22 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
 
   if(R() > 1)
   {
-    if(!cfg->comm_id) return GPU_ACTOR_EINVAL;
-    ncclUniqueId id;
-    memcpy(&id, cfg->comm_id, sizeof(id));
-    NCCLCK(ncclCommInitRank(&g.comm, (int)R(), id, (int)rank()));
     g.xcap = g.cfg.max_exchange ? g.cfg.max_exchange : (1u << 22);
+    if(cfg->comm_id)
+    {
+      ncclUniqueId id;
+      memcpy(&id, cfg->comm_id, sizeof(id));
+      NCCLCK(ncclCommInitRank(&g.comm, (int)R(), id, (int)rank()));
+      g.xp_a2a = nullptr;
+      g.xp_ar = nullptr;
+    }
+    else
+    {
+      // host transport (callbacks registered with gpu_actor_set_transport)
+      if(!g.xp_a2a || !g.xp_ar) return GPU_ACTOR_EINVAL;
+      HIPCK(hipHostMalloc(&g.h_xout, (size_t)R() * g.xcap * sizeof(XRec), hipHostMallocDefault));
+      HIPCK(hipHostMalloc(&g.h_xin, (size_t)R() * g.xcap * sizeof(XRec), hipHostMallocDefault));
+    }
     HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
     HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
     HIPCK(hipMalloc(&g.d_xcount, R() * sizeof(unsigned long long)));
@@ -582,6 +645,19 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
+  g.h_xout = g.h_xin = nullptr;
+  return 0;
+}
+
+GPU_ACTOR_API int gpu_actor_set_transport(gpu_actor_alltoallv_fn alltoallv,
+  gpu_actor_allreduce_fn allreduce, void* ctx)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(g.init) return GPU_ACTOR_ESTATE;
+  if((alltoallv == nullptr) != (allreduce == nullptr)) return GPU_ACTOR_EINVAL;
+  g.xp_a2a = alltoallv;
+  g.xp_ar = allreduce;
+  g.xp_ctx = ctx;
   return 0;
 }
 
@@ -824,6 +900,28 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   int rc = launch_pending(kPendPre);
   if(rc) return rc;
   const unsigned long long* src_stats = g.d_stats;
+  if(R() > 1 && g.xp_ar)
+  {
+    // host transport: sum counters and pending over ranks on the host
+    std::vector<uint64_t> hv(ST_COUNT + 1);
+    HIPCK(hipMemcpyAsync(hv.data(), g.d_stats, ST_COUNT * sizeof(uint64_t),
+      hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipMemcpyAsync(hv.data() + ST_COUNT, g.d_pend + kPendPre, sizeof(uint64_t),
+      hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    if(g.xp_ar(g.xp_ctx, hv.data(), hv.size()) != 0) return GPU_ACTOR_ECOMM;
+    memcpy(st, hv.data(), sizeof(st));
+    memset(out, 0, sizeof(*out));
+    out->steps = g.steps_total;
+    out->delivered = st[ST_DELIVERED];
+    out->sent = st[ST_SENT];
+    out->pending = hv[ST_COUNT];
+    out->dropped = st[ST_DROPPED] + st[ST_XCHG_OVERFLOW];
+    out->remote = g.remote_total;
+    out->active = st[ST_ACTIVE];
+    for(int t = 0; t < GPU_ACTOR_MAX_TYPES; ++t) out->delivered_by_type[t] = st[ST_BY_TYPE + t];
+    return 0;
+  }
   if(R() > 1)
   {
     // sum counters and pending over ranks into scratch (pend[0 .. ST_COUNT))

@@ -140,6 +140,7 @@ struct ActorCtx {
   int      applied_type;
   ORec*     out;         // zone outbox (global scratch)
   uint32_t  ocap;        // its capacity
+  uint32_t  nxt;         // landing parity of this step's sends
   uint32_t* s_nout;      // LDS outbox counter
   uint32_t* s_hist;      // LDS histogram by bucket
   unsigned long long* agg;   // this wave's LDS aggregation word
@@ -173,13 +174,49 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
   (void)beh;
 }
 
+// Outbox full (a zone sent more than its mailbox capacity this step): land the
+// record directly with its own atomic on the destination bucket's counter. The
+// receiver sorts by key, so where a record lands does not change delivery order.
+__device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint32_t w, uint64_t arg)
+{
+  const uint32_t R = c_eng.nranks;
+  const uint32_t nz = c_eng.n_zones;
+  const uint32_t b = bucket_of(to);
+  if(b < nz)
+  {
+    const uint32_t pos = atomicAdd(&c_eng.land_n[a.nxt][b], 1u);
+    if(pos < zone_capacity(b))
+    {
+      uint4 v;
+      v.x = w | ((to / R) & kZoneMask);
+      v.y = a.self;
+      v.z = (uint32_t)arg;
+      v.w = (uint32_t)(arg >> 32);
+      *reinterpret_cast<uint4*>(c_eng.land[a.nxt] + c_eng.zoff[b] + pos) = v;
+    }
+    else
+      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+  }
+  else
+  {
+    const unsigned long long pos = atomicAdd(&c_eng.xcount[b - nz], 1ull);
+    if(pos < c_eng.xcap)
+    {
+      XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
+      x->to = to; x->w = w; x->from = a.self; x->pad = 0; x->arg = arg;
+    }
+    else
+      atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], 1ull);
+  }
+}
+
 // Park one record in the zone outbox and count it in its destination bucket.
 __device__ __forceinline__ void outbox_put(ActorCtx& a, uint32_t to, uint32_t w, uint64_t arg)
 {
   const uint32_t idx = atomicAdd(a.s_nout, 1u);
   if(idx >= a.ocap)
   {
-    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    send_direct(a, to, w, arg);
     return;
   }
   ORec r;

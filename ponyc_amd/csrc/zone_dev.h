@@ -409,6 +409,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   a.out = c_eng.O + c_eng.zoff[z];
   a.s_nout = &s_nout;
   a.ocap = cap;
+  a.nxt = nxt;
   a.s_hist = s_hist;
   a.agg = &s_agg[wv];
   ZRec* Cout = c_eng.carry[nxt] + c_eng.zoff[z];

@@ -77,7 +77,15 @@ EXPORTS = [
     "gpu_actor_run", "gpu_actor_run_fixed", "gpu_actor_sync",
     "gpu_actor_state_read", "gpu_actor_state_write", "gpu_actor_counts",
     "gpu_actor_owner", "gpu_actor_stream", "gpu_actor_last_drain_ms", "gpu_actor_strerror",
+    "gpu_actor_set_transport",
 ]
+
+# host-transport callbacks (include/gpu_actor.h: gpu_actor_alltoallv_fn / _allreduce_fn)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_uint64))
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64)
 
 _lib = None
 
@@ -114,6 +122,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "gpu_actor_stream": (vp, []),
         "gpu_actor_last_drain_ms": (ctypes.c_double, []),
         "gpu_actor_strerror": (ctypes.c_char_p, [i32]),
+        "gpu_actor_set_transport": (i32, [ALLTOALLV_FN, ALLREDUCE_FN, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -121,6 +130,36 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def _wrap_transport(t):
+    """C callbacks around a Python transport; returned so the caller keeps them alive."""
+    def _view(ptr, nbytes):
+        if nbytes == 0 or not ptr:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
+
+    def a2a(_ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            n = t.world_size
+            sb = [int(send_bytes[i]) for i in range(n)]
+            rb = [int(recv_bytes[i]) for i in range(n)]
+            t.alltoallv(_view(send, sum(sb)), sb, _view(recv, sum(rb)), rb)
+            return 0
+        except Exception as e:  # never let an exception cross the C boundary
+            print(f"gpu_actor transport alltoallv failed: {e!r}")
+            return -1
+
+    def ar(_ctx, buf, n):
+        try:
+            arr = np.ctypeslib.as_array(buf, shape=(int(n),))
+            t.allreduce(arr)
+            return 0
+        except Exception as e:
+            print(f"gpu_actor transport allreduce failed: {e!r}")
+            return -1
+
+    return ALLTOALLV_FN(a2a), ALLREDUCE_FN(ar)
 
 
 def _ck(fn: str, rc: int) -> None:
@@ -142,8 +181,16 @@ class Engine:
 
     def __init__(self, device: int = 0, n_ranks: int = 1, rank: int = 0, batch: int = 0,
                  mailbox_cap: int = 0, max_actors: int = 0, max_exchange: int = 0,
-                 comm_id: bytes | None = None):
+                 comm_id: bytes | None = None, transport=None):
+        """`comm_id` selects the RCCL exchange; `transport` (an object with
+        `alltoallv(send, send_bytes, recv, recv_bytes)` and `allreduce(buf)`
+        over numpy arrays, e.g. `ponyc_amd.dist.GlooTransport`) selects the
+        host-staged exchange instead. One of them is required when n_ranks > 1."""
         self.lib = load_library()
+        self._xp = None
+        if transport is not None:
+            self._xp = _wrap_transport(transport)
+            _ck("gpu_actor_set_transport", self.lib.gpu_actor_set_transport(*self._xp, None))
         cfg = Config()
         cfg.device = device
         cfg.n_ranks = n_ranks
@@ -260,6 +307,9 @@ class Engine:
         if self.alive:
             _ck("gpu_actor_shutdown", self.lib.gpu_actor_shutdown())
             self.alive = False
+            if self._xp is not None:  # drop the callbacks before they are freed
+                self.lib.gpu_actor_set_transport(ALLTOALLV_FN(), ALLREDUCE_FN(), None)
+                self._xp = None
 
     def __enter__(self):
         return self

@@ -1,0 +1,79 @@
+"""One rank of a multi-rank parity run (launched by tests/test_multirank.py via
+torch.distributed.run; every rank drives the same GPU through the host
+transport).  Rank 0 runs the CPU oracle on the same workload and prints one
+`MR_RESULT {json}` line: final state, counts and step count must match the
+single-rank BSP restatement bit for bit."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np                       # noqa: E402
+import torch.distributed as dist         # noqa: E402
+
+from ponyc_amd import workloads as W     # noqa: E402
+from ponyc_amd.dist import GlooTransport, GlobalView   # noqa: E402
+from ponyc_amd.engine import Engine      # noqa: E402
+
+CASES = {
+    "ring": (lambda e: W.ring(e, 64, 4, 100), W.ring_result, {}),
+    "ring1": (lambda e: W.ring(e, 1, 3, 7), W.ring_result, {}),
+    "ubench": (lambda e: W.ubench(e, 4096, 4, 32), W.ubench_result, {}),
+    "ubench_det": (lambda e: W.ubench(e, 3001, 3, det=True, hops=40), W.ubench_result, {}),
+    "fanin": (lambda e: W.fanin(e, 5000, 16, 20, 1), W.fanin_result, {}),
+    "gups": (lambda e: W.gups(e, 14, 8, 64, 64, 3), W.gups_result, {}),
+    "storm": (lambda e: W.storm(e, 3000, 4, 12), lambda e, w: e.state_read(w["type"]), {}),
+    "fifo": (lambda e: W.fifo(e, 64, 7, 10, 4, batch=7, mailbox_cap=1024), W.fifo_result, {}),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("case")
+    ap.add_argument("--rccl", action="store_true",
+                    help="use the RCCL exchange (needs one GPU per rank)")
+    ap.add_argument("--same-gpu", action="store_true", help="every rank on device 0")
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    setup, result, kw = CASES[a.case]
+    if a.rccl:
+        from ponyc_amd.dist import share_comm_id
+        lr = 0 if a.same_gpu else int(os.environ.get("LOCAL_RANK", rank))
+        eng = Engine(device=lr, n_ranks=world, rank=rank, comm_id=share_comm_id(Engine), **kw)
+    else:
+        eng = Engine(device=0, n_ranks=world, rank=rank, transport=GlooTransport(), **kw)
+    w = setup(eng)
+    steps = eng.run(0)
+    c = eng.counts()
+    res = result(GlobalView(eng), w)
+    eng.shutdown()
+    if rank == 0:
+        import pyoracle
+        o = pyoracle.Oracle()
+        wo = setup(o)
+        so = o.run(0)
+        co = o.counts()
+        ro = result(o, wo)
+        o.shutdown()
+        out = {
+            "case": a.case, "world": world,
+            "state_equal": bool(np.array_equal(res, ro)),
+            "steps": [int(steps), int(so)],
+            "delivered": [c["delivered"], co["delivered"]],
+            "sent": [c["sent"], co["sent"]],
+            "pending": [c["pending"], co["pending"]],
+            "by_type": c["delivered_by_type"] == co["delivered_by_type"],
+            "dropped": c["dropped"], "remote": c["remote"],
+        }
+        print("MR_RESULT " + json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+"""N>1 path.  CPU: world_size 2 and 3 gloo runs of the host
+plumbing (tests/mr_cpu_worker.py).  GPU: 2 ranks sharing the one GPU of the
+test box through the host-staged exchange (tests/mr_worker.py) — the same
+k_step outbox buckets, xout records, k_xinject landing and counter sums as the
+RCCL exchange, checked bit-exact against the single-rank CPU oracle."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(script, nproc, *args, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           os.path.join(HERE, script), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    return p.stdout
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_host_plumbing_gloo(nproc):
+    assert "MR_CPU_OK" in _launch("mr_cpu_worker.py", nproc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ring", "ring1", "ubench", "ubench_det", "fanin", "gups",
+                                  "storm", "fifo"])
+def test_two_ranks_one_gpu(case):
+    out = _launch("mr_worker.py", 2, case)
+    line = [l for l in out.splitlines() if l.startswith("MR_RESULT ")]
+    assert line, out[-2000:]
+    r = json.loads(line[-1][len("MR_RESULT "):])
+    assert r["dropped"] == 0
+    assert r["state_equal"]
+    assert r["steps"][0] == r["steps"][1]
+    assert r["delivered"][0] == r["delivered"][1]
+    assert r["sent"][0] == r["sent"][1]
+    assert r["pending"][0] == r["pending"][1]
+    assert r["by_type"]
+    assert case == "ring1" or r["remote"] > 0
