@@ -216,6 +216,7 @@ int upload_types()
   memset(&e, 0, sizeof(e));
   e.n_types = g.n_types; e.rank = rank(); e.nranks = R(); e.n_local = g.n_local;
   e.n_zones = g.n_zones; e.zoff = g.d_zoff; e.zcapz = g.d_zcap;
+  e.r_magic = R() > 1 ? ~0ull / R() + 1 : 0;
   for(int p = 0; p < 2; ++p)
   {
     e.land[p] = g.d_land[p]; e.carry[p] = g.d_carry[p];
@@ -420,13 +421,38 @@ int exchange(uint32_t land_par)
   return 0;
 }
 
+// k_step compiled for the one handler table all serial actors share, when
+// they do (smaller code, no spills); the any-mix instantiation otherwise.
+typedef void (*step_kernel_t)(uint32_t, uint32_t);
+step_kernel_t pick_step_kernel()
+{
+  int only = -1;
+  for(const HostType& t : g.types)
+  {
+    if(!t.created || reducible_ht(t.ht)) continue;
+    if(only >= 0 && (uint32_t)only != t.ht) return k_step<-1>;
+    only = (int)t.ht;
+  }
+  switch(only)
+  {
+    case GPU_ACTOR_HT_RING: return k_step<GPU_ACTOR_HT_RING>;
+    case GPU_ACTOR_HT_PINGER: return k_step<GPU_ACTOR_HT_PINGER>;
+    case GPU_ACTOR_HT_PINGER_DET: return k_step<GPU_ACTOR_HT_PINGER_DET>;
+    case GPU_ACTOR_HT_FANIN_SENDER: return k_step<GPU_ACTOR_HT_FANIN_SENDER>;
+    case GPU_ACTOR_HT_GUPS_STREAMER: return k_step<GPU_ACTOR_HT_GUPS_STREAMER>;
+    case GPU_ACTOR_HT_STORM: return k_step<GPU_ACTOR_HT_STORM>;
+    default: return k_step<-1>;
+  }
+}
+
 // One superstep: k_step on parity g.par (+ exchange), then flip parity.
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
   if(e0) HIPCK(hipEventRecord(e0, g.stream));
   const size_t dyn = 2 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
-  hipLaunchKernelGGL(k_step, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
+  step_kernel_t kern = pick_step_kernel();
+  hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
   if(e1) HIPCK(hipEventRecord(e1, g.stream));
   HIPCK(hipGetLastError());
   g.par ^= 1u;

@@ -77,6 +77,7 @@ struct TypeDev {
 struct EngDev {
   uint32_t n_types, rank, nranks, n_local;
   uint32_t n_zones, pad0;
+  uint64_t r_magic;               // floor(2^64 / nranks) + 1 (nranks > 1): rdiv
   const uint64_t* zoff;           // [n_zones] record offset of each zone's buffers
   const uint32_t* zcapz;          // [n_zones] records a zone buffer holds
   ZRec* land[2];                  // zone z: [zoff[z], zoff[z] + zcapz[z])
@@ -95,6 +96,18 @@ struct EngDev {
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
 __constant__ EngDev  c_eng;
+
+// x / nranks and x % nranks without a division instruction sequence: for
+// 32-bit x, mulhi(x, floor(2^64 / d) + 1) is exact (Lemire's fastdiv).
+__device__ __forceinline__ uint32_t rdiv(uint32_t x)
+{
+  return c_eng.nranks == 1 ? x : (uint32_t)__umul64hi(c_eng.r_magic, (uint64_t)x);
+}
+
+__device__ __forceinline__ uint32_t rmod(uint32_t x)
+{
+  return x - rdiv(x) * c_eng.nranks;
+}
 
 __device__ __forceinline__ int type_of_local(uint32_t L)
 {
@@ -123,10 +136,10 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t to)
   const uint32_t R = c_eng.nranks;
   if(R > 1)
   {
-    const uint32_t owner = to % R;
+    const uint32_t owner = rmod(to);
     if(owner != c_eng.rank) return c_eng.n_zones + owner;
   }
-  return (to / R) >> kZoneBits;
+  return rdiv(to) >> kZoneBits;
 }
 
 // Per-lane bookkeeping while one actor drains.
@@ -154,7 +167,7 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
   const int t = type_of_global(to);
   if(t < 0) return;
   const TypeDev& T = c_types[t];
-  const uint32_t li = to / c_eng.nranks - T.lfirst;
+  const uint32_t li = rdiv(to) - T.lfirst;
   switch(T.ht)
   {
     case GPU_ACTOR_HT_FANIN_ANALYZER:
@@ -188,7 +201,7 @@ __device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint
     if(pos < zone_capacity(b))
     {
       uint4 v;
-      v.x = w | ((to / R) & kZoneMask);
+      v.x = w | (rdiv(to) & kZoneMask);
       v.y = a.self;
       v.z = (uint32_t)arg;
       v.w = (uint32_t)(arg >> 32);
@@ -240,7 +253,7 @@ __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t b
 
 __device__ __forceinline__ bool is_remote(uint32_t to)
 {
-  return c_eng.nranks > 1 && to % c_eng.nranks != c_eng.rank;
+  return c_eng.nranks > 1 && rmod(to) != c_eng.rank;
 }
 
 // fan-in Analyzer apply, aggregated per wavefront: lanes hitting the same
@@ -276,7 +289,7 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
       if(t >= 0)
       {
         const TypeDev& T = c_types[t];
-        const uint32_t li = tl / c_eng.nranks - T.lfirst;
+        const uint32_t li = rdiv(tl) - T.lfirst;
         atomicAdd(reinterpret_cast<unsigned long long*>(&T.state[li]),
           (unsigned long long)__popcll(peers));
         atomicXor(reinterpret_cast<unsigned long long*>(&T.state[(size_t)T.lcount + li]),

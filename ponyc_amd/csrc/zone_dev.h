@@ -36,6 +36,10 @@ namespace gpa {
 constexpr int kUnroll = 8;   // independent records in flight per thread in streaming loops
 constexpr int kScatterUnroll = 4;     // outbox records in flight per thread in the scatter
 constexpr uint32_t kIdxCap = 16384;   // LDS index budget per zone (records per step)
+#ifndef GPA_SMALL
+#define GPA_SMALL 16
+#endif
+constexpr uint32_t kSmall = GPA_SMALL;  // arrival groups up to this size are ordered in registers
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
@@ -171,13 +175,14 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Ac
   if(g > 0)
   {
     const uint32_t q = w - done;
-    if(q >= g && g <= 8)
+    if(q >= g && g <= kSmall)
     {
       // small group handled whole: all records in registers, select by key
-      uint64_t k[8], v[8];
-      uint32_t bh[8];
+      bool g_done = false;
+      uint64_t k[kSmall], v[kSmall];
+      uint32_t bh[kSmall];
 #pragma unroll
-      for(int j = 0; j < 8; ++j)
+      for(int j = 0; j < (int)kSmall; ++j)
       {
         if((uint32_t)j < g)
         {
@@ -189,15 +194,28 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Ac
           k[j] = ~0ull; v[j] = 0; bh[j] = 0;
         }
       }
-      for(uint32_t r = 0; r < g; ++r)
+#ifdef GPA_SAME_SMALL
+      // A handler sees only (behaviour, arg): when every record of the group
+      // carries the same pair, any order of them is the canonical one.
+      bool same = true;
+#pragma unroll
+      for(int j = 1; j < (int)kSmall; ++j)
+        if((uint32_t)j < g) same = same && v[j] == v[0] && bh[j] == bh[0];
+      if(same)
+      {
+        for(uint32_t r = 0; r < g; ++r) handle<HT>(T, a, s, bh[0], v[0], nullptr);
+        g_done = true;
+      }
+#endif
+      for(uint32_t r = 0; r < g && !g_done; ++r)
       {
         uint64_t best = k[0], barg = v[0];
         uint32_t bb = bh[0], bi = 0;
 #pragma unroll
-        for(int j = 1; j < 8; ++j)
+        for(int j = 1; j < (int)kSmall; ++j)
           if(k[j] < best) { best = k[j]; barg = v[j]; bb = bh[j]; bi = (uint32_t)j; }
 #pragma unroll
-        for(int j = 0; j < 8; ++j)
+        for(int j = 0; j < (int)kSmall; ++j)
           if((uint32_t)j == bi) k[j] = ~0ull;
         handle<HT>(T, a, s, bb, barg, nullptr);
       }
@@ -207,7 +225,22 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Ac
     {
       // large group handled whole: select in key order
       uint64_t last = 0;
-      for(uint32_t r = 0; r < g; ++r)
+      bool same = false;
+#ifdef GPA_SAME_LARGE
+      {
+        const ZRec r0 = acc.rec(nc);
+        const uint32_t w0 = r0.w0 & 0xF000u;
+        same = true;
+        for(uint32_t j = 1; j < g && same; ++j)
+        {
+          const ZRec rj = acc.rec(nc + j);
+          same = rj.arg == r0.arg && (rj.w0 & 0xF000u) == w0;
+        }
+        if(same)
+          for(uint32_t r = 0; r < g; ++r) handle<HT>(T, a, s, w0 >> 12, r0.arg, nullptr);
+      }
+#endif
+      for(uint32_t r = 0; r < g && !same; ++r)
       {
         uint64_t best = ~0ull;
         uint32_t bi = 0;
@@ -254,6 +287,9 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Ac
 }
 
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
+// HTS >= 0: every serial actor of this engine runs handler table HTS (the host
+// checks), so only that table is compiled in; HTS < 0: any mix of tables.
+template <int HTS>
 __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot)
 {
   __shared__ uint32_t s_cnt[kZone];     // records per actor this step
@@ -386,15 +422,30 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __syncthreads();
   GPA_STAMP(3);
 
+  // The zone's type when one type covers all of its slots, else -1. It is
+  // wave-uniform, so that type's fields (batch, state, params) come through
+  // scalar loads instead of a per-lane lookup chain.
+  int tz = -1;
+  for(uint32_t t = 0; t < c_eng.n_types; ++t)
+    if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
+      tz = (int)t;
+  tz = __builtin_amdgcn_readfirstlane(tz);
+
   // carry-out sizes (known before any handler runs) -> offsets
+  const uint32_t zbatch = tz >= 0 ? c_types[tz].batch : 0u;
   for(uint32_t i = tid; i < kZone; i += kZoneThreads)
   {
     uint32_t rem = 0;
     const uint32_t n = s_cnt[i];
     if(i < nact && n)
     {
-      const int t = type_of_local(L0 + i);
-      if(t >= 0) rem = n > c_types[t].batch ? n - c_types[t].batch : 0u;
+      uint32_t bt = zbatch;
+      if(tz < 0)
+      {
+        const int t = type_of_local(L0 + i);
+        bt = t >= 0 ? c_types[t].batch : ~0u;
+      }
+      rem = n > bt ? n - bt : 0u;
     }
     s_aux[i] = rem;
   }
@@ -414,14 +465,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   a.agg = &s_agg[wv];
   ZRec* Cout = c_eng.carry[nxt] + c_eng.zoff[z];
   uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
-  for(uint32_t i = tid; i < nact; i += kZoneThreads)
-  {
+  // drain local actor i, of type t (T = c_types[t])
+  auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
     const uint32_t n = s_cnt[i];
-    if(n == 0) continue;
     const uint32_t L = L0 + i;
-    const int t = type_of_local(L);
-    if(t < 0 || c_types[t].reducible) continue;
-    const TypeDev& T = c_types[t];
     a.li = L - T.lfirst;
     a.self = L * R + me;
     a.src_local = i;
@@ -429,32 +476,59 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     const uint32_t co = s_aux[i];
     const uint32_t room = co < cap ? cap - co : 0u;
     uint32_t d = 0;
-    switch(T.ht)
+#define ZDRAIN(HT)                                                                    \
+    if(use_idx)                                                                       \
+    {                                                                                 \
+      AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                        \
+      d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], Cout + co, room);                   \
+    }                                                                                 \
+    else                                                                              \
+      d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], Cout + co, room);
+    if constexpr(HTS >= 0)
     {
-#define ZCASE(HT)                                                                     \
-      case HT:                                                                          \
-        if(use_idx)                                                                     \
-        {                                                                               \
-          AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                      \
-          d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], Cout + co, room);                 \
-        }                                                                               \
-        else                                                                            \
-          d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], Cout + co, room); \
-        break;
-      ZCASE(GPU_ACTOR_HT_RING)
-      ZCASE(GPU_ACTOR_HT_PINGER)
-      ZCASE(GPU_ACTOR_HT_PINGER_DET)
-      ZCASE(GPU_ACTOR_HT_FANIN_SENDER)
-      ZCASE(GPU_ACTOR_HT_GUPS_STREAMER)
-      ZCASE(GPU_ACTOR_HT_STORM)
-      ZCASE(GPU_ACTOR_HT_FIFO_SRC)
-      ZCASE(GPU_ACTOR_HT_FIFO_SINK)
-#undef ZCASE
-      default: break;
+      ZDRAIN(HTS)
     }
+    else
+    {
+      switch(T.ht)
+      {
+#define ZCASE(HT) case HT: { ZDRAIN(HT) } break;
+        ZCASE(GPU_ACTOR_HT_RING)
+        ZCASE(GPU_ACTOR_HT_PINGER)
+        ZCASE(GPU_ACTOR_HT_PINGER_DET)
+        ZCASE(GPU_ACTOR_HT_FANIN_SENDER)
+        ZCASE(GPU_ACTOR_HT_GUPS_STREAMER)
+        ZCASE(GPU_ACTOR_HT_STORM)
+        ZCASE(GPU_ACTOR_HT_FIFO_SRC)
+        ZCASE(GPU_ACTOR_HT_FIFO_SINK)
+#undef ZCASE
+        default: break;
+      }
+    }
+#undef ZDRAIN
     delivered += d;
     active += d ? 1u : 0u;
-    if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
+    return d;
+  };
+  if(tz >= 0)
+  {
+    const TypeDev& T = c_types[tz];
+    uint32_t dz = 0;
+    if(!T.reducible)
+      for(uint32_t i = tid; i < nact; i += kZoneThreads)
+        if(s_cnt[i]) dz += drain_actor(T, tz, i);
+    if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
+  }
+  else
+  {
+    for(uint32_t i = tid; i < nact; i += kZoneThreads)
+    {
+      if(s_cnt[i] == 0) continue;
+      const int t = type_of_local(L0 + i);
+      if(t < 0 || c_types[t].reducible) continue;
+      const uint32_t d = drain_actor(c_types[t], t, i);
+      if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
+    }
   }
   sent = a.sent;
   applied = a.applied;
@@ -512,7 +586,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         if(pos[u] < zone_capacity(b[u]))
         {
           uint4 v;
-          v.x = (ov[u].y & ~kZoneMask) | ((ov[u].x / R) & kZoneMask);
+          v.x = (ov[u].y & ~kZoneMask) | (rdiv(ov[u].x) & kZoneMask);
           v.y = from;
           v.z = ov[u].z;
           v.w = ov[u].w;
@@ -588,7 +662,7 @@ __device__ __forceinline__ void land_block(bool valid, uint32_t to, uint32_t w_n
   uint32_t zt = 0;
   if(valid)
   {
-    zt = (to / c_eng.nranks) >> kZoneBits;
+    zt = rdiv(to) >> kZoneBits;
     atomicAdd(&s_hist[zt], 1u);
   }
   __syncthreads();
@@ -604,7 +678,7 @@ __device__ __forceinline__ void land_block(bool valid, uint32_t to, uint32_t w_n
     if(pos < zone_capacity(zt))
     {
       ZRec r;
-      r.w0 = w_noto | ((to / c_eng.nranks) & kZoneMask);
+      r.w0 = w_noto | (rdiv(to) & kZoneMask);
       r.from = from;
       r.arg = arg;
       *reinterpret_cast<uint4*>(c_eng.land[cur] + c_eng.zoff[zt] + pos) =

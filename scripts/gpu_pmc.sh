@@ -1,12 +1,30 @@
-# PMC passes for the step kernel (separate passes: FETCH_SIZE, WRITE_SIZE, L2 hit)
+# PMC passes for the step kernel, one rocprofv3 run per pass (separate --pmc
+# runs, kernel-trace only; MI355X_MICROARCH.md HBM/rocprofv3 section).
+# Counters missing from `rocprofv3 -L` on the box are dropped from a pass.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
 TAG=${TAG:-r01}
-rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
-for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
-  N=$(echo $C | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc/${TAG}_$N -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/pmc/bench_$N.json 2> gpurun_out/pmc/err_$N.txt || exit $?
-done
-ls -R gpurun_out/pmc | head -40
+OUT=gpurun_out/pmc_$TAG
+mkdir -p $OUT
+timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || exit $?
+have() { grep -qw "$1" $OUT/counters_list.txt; }
+i=0
+while read -r line; do
+  [ -z "$line" ] && continue
+  sel=""
+  for c in $line; do base=${c%_sum}; if have $c || have $base; then sel="$sel $c"; fi; done
+  [ -z "$sel" ] && continue
+  i=$((i+1))
+  echo "pass $i:$sel"
+  timeout -s KILL 90 rocprofv3 --pmc $sel --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
+    python3 bench.py --no-cpu-baseline --steps 6 --warmup 2 > $OUT/bench_p$i.json 2> $OUT/err_p$i.txt || exit $?
+done <<'PASSES'
+FETCH_SIZE
+WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT
+TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_REQ_sum
+TA_BUSY_avr TA_TA_BUSY_sum TD_BUSY_avr
+PASSES
+find $OUT -name '*counter_collection.csv' | sort
