@@ -450,7 +450,7 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
   if(e0) HIPCK(hipEventRecord(e0, g.stream));
-  const size_t dyn = 2 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
+  const size_t dyn = 4 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
   step_kernel_t kern = pick_step_kernel();
   hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
   if(e1) HIPCK(hipEventRecord(e1, g.stream));

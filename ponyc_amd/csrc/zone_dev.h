@@ -34,8 +34,10 @@ namespace gpa {
 #endif
 
 constexpr int kUnroll = 8;   // independent records in flight per thread in streaming loops
-constexpr int kScatterUnroll = 4;     // outbox records in flight per thread in the scatter
 constexpr uint32_t kIdxCap = 16384;   // LDS index budget per zone (records per step)
+constexpr uint32_t kTile = 4096;      // outbox records sorted per scatter tile (64 KB of LDS)
+constexpr int kTilePer = kTile / 512; // tile records per thread
+constexpr int kIdxPer = kIdxCap / 512; // landed records per thread on the LDS-index path
 #ifndef GPA_SMALL
 #define GPA_SMALL 16
 #endif
@@ -83,6 +85,33 @@ __device__ uint32_t block_scan_zone(uint32_t* arr, uint32_t* s_tmp)
   uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
 #pragma unroll
   for(uint32_t k = 0; k < per; ++k) { arr[tid * per + k] = run; run += v[k]; }
+  const uint32_t total = s_tmp[kZoneWaves - 1];
+  __syncthreads();
+  return total;
+}
+
+// Exclusive scan of in[0, n) into out[0, n) (LDS) by a kZoneThreads workgroup,
+// each thread taking a contiguous run; returns the total. All threads call it;
+// it ends behind a barrier.
+__device__ uint32_t block_scan_n(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* s_tmp)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t per = (n + kZoneThreads - 1) / kZoneThreads;
+  const uint32_t lo = min(tid * per, n), hi = min(lo + per, n);
+  uint32_t sum = 0;
+  for(uint32_t i = lo; i < hi; ++i) sum += in[i];
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  if(lane == 63) s_tmp[wv] = incl;
+  __syncthreads();
+  if(wv == 0)
+  {
+    uint32_t x = lane < (uint32_t)kZoneWaves ? s_tmp[lane] : 0u;
+    x = wave_incl_scan(x, lane);
+    if(lane < (uint32_t)kZoneWaves) s_tmp[lane] = x;
+  }
+  __syncthreads();
+  uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
+  for(uint32_t i = lo; i < hi; ++i) { const uint32_t v = in[i]; out[i] = run; run += v; }
   const uint32_t total = s_tmp[kZoneWaves - 1];
   __syncthreads();
   return total;
@@ -155,45 +184,56 @@ struct AccS {
 // arrival group in (from, seq) key order — and hand the canonical tail to the
 // next step's carry buffer.
 template <int HT, class Acc>
-__device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Acc acc,
+__device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a, Acc acc,
   uint32_t n, uint32_t nc, ZRec* cout, uint32_t cout_room)
 {
+  // a register copy of the type's fields: read once, not re-read after every
+  // store the handlers make (the compiler cannot prove they do not alias)
+  const TypeDev T = Tref;
   constexpr int NW = HT_Words<HT>::W;
   const uint32_t w = n < T.batch ? n : T.batch;
   uint64_t s[NW];
 #pragma unroll
   for(int k = 0; k < NW; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
+  const uint32_t g = n - nc;
+  const uint32_t hc = min(w, nc);                 // carried messages handled now
+  const bool small = g > 0 && w - hc >= g && g <= kSmall;
+  // small arrival group: its records are loaded with the state, before any
+  // handler runs (one round of memory latency for the actor)
+  uint64_t k[kSmall], v[kSmall];
+  uint32_t bh[kSmall];
+#pragma unroll
+  for(int j = 0; j < (int)kSmall; ++j)
+  {
+    if(small && (uint32_t)j < g)
+    {
+      const ZRec r = acc.rec(nc + j);
+      k[j] = zkey(r); v[j] = r.arg; bh[j] = (r.w0 >> 12) & 0xFu;
+    }
+    else
+    {
+      k[j] = ~0ull; v[j] = 0; bh[j] = 0;
+    }
+  }
+  // Wait for those loads here, once: otherwise the wait lands at the head of
+  // the handler loops, where it also waits for every outbox store the previous
+  // message made (vmcnt counts stores too).
+  __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
   uint32_t done = 0;
-  while(done < w && done < nc)
+  while(done < hc)
   {
     const ZRec r = acc.rec(done);
     handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
     ++done;
   }
-  const uint32_t g = n - nc;
   bool sorted_tail = true;
   if(g > 0)
   {
     const uint32_t q = w - done;
-    if(q >= g && g <= kSmall)
+    if(small)
     {
       // small group handled whole: all records in registers, select by key
       bool g_done = false;
-      uint64_t k[kSmall], v[kSmall];
-      uint32_t bh[kSmall];
-#pragma unroll
-      for(int j = 0; j < (int)kSmall; ++j)
-      {
-        if((uint32_t)j < g)
-        {
-          const ZRec r = acc.rec(nc + j);
-          k[j] = zkey(r); v[j] = r.arg; bh[j] = (r.w0 >> 12) & 0xFu;
-        }
-        else
-        {
-          k[j] = ~0ull; v[j] = 0; bh[j] = 0;
-        }
-      }
 #ifdef GPA_SAME_SMALL
       // A handler sees only (behaviour, arg): when every record of the group
       // carries the same pair, any order of them is the canonical one.
@@ -292,12 +332,17 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& T, ActorCtx& a, Ac
 template <int HTS>
 __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot)
 {
-  __shared__ uint32_t s_cnt[kZone];     // records per actor this step
-  __shared__ uint32_t s_off[kZone];     // segment offset in S
-  __shared__ uint32_t s_ccnt[kZone];    // carried records per actor
-  __shared__ uint32_t s_aux[kZone];     // carry start -> landing cursor -> carry-out offset
-  __shared__ uint16_t s_idx[kIdxCap];   // per-actor segments: index into carry ++ landing
-  extern __shared__ uint32_t s_dyn[];       // [nb] histogram, [nb] chunk bases
+  // 64 KB pool. Phases 1-3: per-actor arrays + the segment index; phase 4:
+  // the outbox sort tile (kTile records).
+  __shared__ uint4 s_pool[kTile];
+  static_assert(4 * kZone * sizeof(uint32_t) + kIdxCap * sizeof(uint16_t) <= sizeof(uint4) * kTile,
+                "LDS pool too small");
+  uint32_t* const s_cnt = reinterpret_cast<uint32_t*>(s_pool);   // records per actor this step
+  uint32_t* const s_off = s_cnt + kZone;    // segment offset in S
+  uint32_t* const s_ccnt = s_off + kZone;   // carried records per actor
+  uint32_t* const s_aux = s_ccnt + kZone;   // carry start -> landing cursor -> carry-out offset
+  uint16_t* const s_idx = reinterpret_cast<uint16_t*>(s_aux + kZone);  // index into carry ++ landing
+  extern __shared__ uint32_t s_dyn[];   // [nb] histogram, [nb] chunk bases, [nb] tile counts, [nb] tile starts
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
   __shared__ uint32_t s_nout;
   __shared__ unsigned long long s_agg[kZoneWaves];
@@ -327,13 +372,32 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t nl = min(c_eng.land_n[cur][z], cap);
   const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
   const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
+  const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
+  // carried records counted apart (s_ccnt); landed ones in s_cnt
   for(uint32_t i = tid; i < nc; i += kZoneThreads)
+    atomicAdd(&s_ccnt[C[i].w0 & kZoneMask], 1u);
+  // Landed records: with the LDS index, each record's rank among its actor's
+  // arrivals comes back from the counting atomic and stays in a register
+  // (packed rank << 11 | actor), so placing it needs no second pass over the
+  // landing buffer. kIdxPer loads in flight per thread.
+  uint32_t wr[kIdxPer];
+  if(use_idx)
   {
-    const uint32_t a = C[i].w0 & kZoneMask;
-    atomicAdd(&s_cnt[a], 1u);
-    atomicAdd(&s_ccnt[a], 1u);
+#pragma unroll
+    for(int u = 0; u < kIdxPer; ++u)
+    {
+      const uint32_t i = u * kZoneThreads + tid;
+      wr[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for(int u = 0; u < kIdxPer; ++u)
+      if(wr[u] != 0xFFFFFFFFu)
+      {
+        const uint32_t act = wr[u] & kZoneMask;
+        wr[u] = (atomicAdd(&s_cnt[act], 1u) << kZoneBits) | act;
+      }
   }
-  // 8 independent loads in flight per thread before their LDS atomics
+  else
   for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
   {
     uint32_t w[kUnroll];
@@ -355,7 +419,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.carry_n[cur][z] = 0;
     c_eng.land_n[cur][z] = 0;
   }
-  for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_off[i] = s_cnt[i]; s_aux[i] = s_ccnt[i]; }
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_off[i] = s_cnt[i] + s_ccnt[i]; s_aux[i] = s_ccnt[i]; }
   __syncthreads();
   (void)block_scan_zone(s_off, s_tmp);
   (void)block_scan_zone(s_aux, s_tmp);
@@ -363,7 +427,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
   ZRec* Sz = c_eng.S + 2 * c_eng.zoff[z];
-  const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
   for(uint32_t i = tid; i < nc; i += kZoneThreads)
   {
     const ZRec r = C[i];
@@ -371,54 +434,47 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     if(use_idx) s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
     else Sz[s_off[a] + (i - s_aux[a])] = r;
   }
-  __syncthreads();
-  for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
-  __syncthreads();
   if(use_idx)
   {
     // LDS index only: records stay in the landing buffer
+#pragma unroll
+    for(int u = 0; u < kIdxPer; ++u)
+      if(wr[u] != 0xFFFFFFFFu)
+      {
+        const uint32_t act = wr[u] & kZoneMask;
+        s_idx[s_off[act] + s_ccnt[act] + (wr[u] >> kZoneBits)] = (uint16_t)(nc + u * kZoneThreads + tid);
+      }
+  }
+  else
+  {
+    __syncthreads();
+    for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
+    __syncthreads();
     for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
     {
-      uint32_t w[kUnroll];
+      uint4 r[kUnroll];
+      uint32_t pos[kUnroll];
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
       {
         const uint32_t i = base + u * kZoneThreads + tid;
-        w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
+        if(i < nl) r[u] = *reinterpret_cast<const uint4*>(Ld + i);
+        else r[u].x = 0xFFFFFFFFu;
       }
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
       {
-        if(w[u] == 0xFFFFFFFFu) continue;
-        const uint32_t a = w[u] & kZoneMask;
-        s_idx[s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u)] =
-          (uint16_t)(nc + base + u * kZoneThreads + tid);
+        if(r[u].x == 0xFFFFFFFFu) continue;
+        const uint32_t a = r[u].x & kZoneMask;
+        pos[u] = s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u);
       }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+        if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
     }
   }
-  else
-  for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
-  {
-    uint4 r[kUnroll];
-    uint32_t pos[kUnroll];
-#pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-    {
-      const uint32_t i = base + u * kZoneThreads + tid;
-      if(i < nl) r[u] = *reinterpret_cast<const uint4*>(Ld + i);
-      else r[u].x = 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-    {
-      if(r[u].x == 0xFFFFFFFFu) continue;
-      const uint32_t a = r[u].x & kZoneMask;
-      pos[u] = s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u);
-    }
-#pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-      if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
-  }
+  // from here on s_cnt is the actor's total: carried + landed
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_cnt[i] += s_ccnt[i];
   __syncthreads();
   GPA_STAMP(3);
 
@@ -540,6 +596,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     atomicAdd(&c_eng.stats[ST_BY_TYPE + tid], s_bytype[tid]);
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
+  uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
+  uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
   for(uint32_t b = tid; b < nb; b += kZoneThreads)
   {
     const uint32_t h = s_hist[b];
@@ -550,63 +608,87 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       else
         s_base[b] = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
     }
-    s_hist[b] = 0;
+    s_tcnt[b] = 0;
   }
   __syncthreads();
   GPA_STAMP(5);
+  // Scatter in tiles sorted by bucket (LDS counting sort), so that a wave's
+  // store instruction writes runs of consecutive records of one chunk rather
+  // than 64 records to 64 chunks (measured 1.75x for a whole-zone sort,
+  // scripts/ubench_scatter.hip).
   const uint32_t nout = min(s_nout, cap);
   const ORec* Oz = c_eng.O + c_eng.zoff[z];
   uint32_t dropped = 0, xover = 0;
-  for(uint32_t base = 0; base < nout; base += kZoneThreads * kScatterUnroll)
+  for(uint32_t t0 = 0; t0 < nout; t0 += kTile)
   {
-    // ov = {to, w, arg lo, arg hi}
-    uint4 ov[kScatterUnroll];
-    uint32_t b[kScatterUnroll], pos[kScatterUnroll];
+    const uint32_t m = min(kTile, nout - t0);
+    uint4 ov[kTilePer];
+    uint32_t bk[kTilePer], rk[kTilePer];
 #pragma unroll
-    for(int u = 0; u < kScatterUnroll; ++u)
+    for(int u = 0; u < kTilePer; ++u)
     {
-      const uint32_t i = base + u * kZoneThreads + tid;
-      if(i < nout) ov[u] = *reinterpret_cast<const uint4*>(Oz + i);
-      else ov[u].y = 0xFFFFFFFFu;
+      const uint32_t i = u * kZoneThreads + tid;
+      if(i < m) ov[u] = *reinterpret_cast<const uint4*>(Oz + t0 + i);
     }
 #pragma unroll
-    for(int u = 0; u < kScatterUnroll; ++u)
+    for(int u = 0; u < kTilePer; ++u)
     {
-      if(ov[u].y == 0xFFFFFFFFu) continue;
-      b[u] = bucket_of(ov[u].x);
-      pos[u] = s_base[b[u]] + atomicAdd(&s_hist[b[u]], 1u);
-    }
-#pragma unroll
-    for(int u = 0; u < kScatterUnroll; ++u)
-    {
-      if(ov[u].y == 0xFFFFFFFFu) continue;
-      const uint32_t from = (L0 + (ov[u].y & kZoneMask)) * R + me;
-      if(b[u] < nz)
+      const uint32_t i = u * kZoneThreads + tid;
+      if(i < m)
       {
-        if(pos[u] < zone_capacity(b[u]))
+        bk[u] = bucket_of(ov[u].x);
+        rk[u] = atomicAdd(&s_tcnt[bk[u]], 1u);
+      }
+    }
+    __syncthreads();
+    (void)block_scan_n(s_tcnt, s_tst, nb, s_tmp);
+#pragma unroll
+    for(int u = 0; u < kTilePer; ++u)
+    {
+      const uint32_t i = u * kZoneThreads + tid;
+      if(i < m) s_pool[s_tst[bk[u]] + rk[u]] = ov[u];
+    }
+    __syncthreads();
+    for(uint32_t p = tid; p < m; p += kZoneThreads)
+    {
+      // r = {to, w, arg lo, arg hi}
+      const uint4 r = s_pool[p];
+      const uint32_t b = bucket_of(r.x);
+      const uint32_t pos = s_base[b] + (p - s_tst[b]);
+      const uint32_t from = (L0 + (r.y & kZoneMask)) * R + me;
+      if(b < nz)
+      {
+        if(pos < zone_capacity(b))
         {
           uint4 v;
-          v.x = (ov[u].y & ~kZoneMask) | (rdiv(ov[u].x) & kZoneMask);
+          v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
           v.y = from;
-          v.z = ov[u].z;
-          v.w = ov[u].w;
-          *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b[u]] + pos[u]) = v;
+          v.z = r.z;
+          v.w = r.w;
+          *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos) = v;
         }
         else
           ++dropped;
       }
       else
       {
-        if(pos[u] < c_eng.xcap)
+        if(pos < c_eng.xcap)
         {
-          XRec* x = c_eng.xout + (size_t)(b[u] - nz) * c_eng.xcap + pos[u];
-          x->to = ov[u].x; x->w = ov[u].y & ~kZoneMask; x->from = from; x->pad = 0;
-          x->arg = ((uint64_t)ov[u].w << 32) | ov[u].z;
+          XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
+          x->to = r.x; x->w = r.y & ~kZoneMask; x->from = from; x->pad = 0;
+          x->arg = ((uint64_t)r.w << 32) | r.z;
         }
         else
           ++xover;
       }
     }
+    __syncthreads();
+    for(uint32_t b = tid; b < nb; b += kZoneThreads)
+    {
+      s_base[b] += s_tcnt[b];
+      s_tcnt[b] = 0;
+    }
+    __syncthreads();
   }
 
   // ---- counters: block reduction, one atomic per workgroup per counter ---------------
