@@ -58,6 +58,8 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PONYC_AMD_SAME_GPU"):      # rehearsal: every rank on device 0
+        local = 0
     pg = None
     if world > 1:
         import torch.distributed as dist
@@ -223,8 +225,8 @@ def main():
             "dtype": "u64",
             "data": "synthetic (seeded xoroshiro128+ pingers)",
             "config": {
-                "workload": "message-ubench C2: 1,048,576 pingers per GPU x 5 initial pings, "
-                            "steady state",
+                "workload": f"message-ubench C2: {args.actors:,} pingers per GPU x "
+                            f"{args.initial} initial pings, steady state",
                 "actors_per_gpu": args.actors, "actors_total": n_total,
                 "initial_pings": args.initial, "mailbox_cap": args.mailbox_cap, "batch": 100,
                 "parallelism": f"actor hash partition x{world} (id % {world})",

@@ -413,7 +413,7 @@ int exchange(uint32_t land_par)
   g.remote_total += total;
   if(total)
   {
-    hipLaunchKernelGGL(k_xinject, dim3(blocks_for(total)), dim3(kBlock), 0, g.stream,
+    hipLaunchKernelGGL(k_xinject, dim3(blocks_for(total, kLandRecs)), dim3(kLandThreads), 0, g.stream,
       (const XRec*)g.d_xin, total, land_par);
     HIPCK(hipGetLastError());
   }
@@ -548,7 +548,7 @@ int sendv_locked(const gpu_msg_t* first, uint64_t n)
   HIPCK(hipMemcpyAsync(g.d_msgs, first, n * sizeof(gpu_msg_t), hipMemcpyHostToDevice, g.stream));
   if(g.n_zones)
   {
-    hipLaunchKernelGGL(k_inject, dim3(blocks_for(n)), dim3(kBlock), 0, g.stream,
+    hipLaunchKernelGGL(k_inject, dim3(blocks_for(n, kLandRecs)), dim3(kLandThreads), 0, g.stream,
       (const gpu_msg_t*)g.d_msgs, n, g.host_seq, g.par);
     HIPCK(hipGetLastError());
   }

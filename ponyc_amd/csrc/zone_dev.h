@@ -733,110 +733,130 @@ __global__ void __launch_bounds__(kBlock) k_pending(uint32_t cur, uint32_t slot)
   }
 }
 
-// Block-aggregated landing of records addressed to this rank's serial actors:
-// one atomicAdd per (block, zone). Used for host sends and cross-rank records.
-__device__ __forceinline__ void land_block(bool valid, uint32_t to, uint32_t w_noto, uint32_t from,
-  uint64_t arg, uint32_t cur, uint32_t* s_hist, uint32_t* s_base)
+// Landing of records addressed to this rank's serial actors (host sends,
+// records from other ranks): a block of kLandThreads threads takes
+// kLandPer records each, counts them per destination zone in LDS, reserves one
+// chunk per (block, zone) with a single atomicAdd, and writes them into it —
+// ~kLandThreads * kLandPer / n_zones records per atomic instead of one.
+constexpr int kLandThreads = 1024;
+constexpr int kLandPer = 8;
+constexpr uint32_t kLandRecs = kLandThreads * kLandPer;
+
+struct LandRec {
+  bool valid;
+  uint32_t to, w, from;
+  uint64_t arg;
+};
+
+__device__ __forceinline__ void land_records(LandRec (&r)[kLandPer], uint32_t cur,
+  uint32_t* s_hist, uint32_t* s_base)
 {
   const uint32_t nz = c_eng.n_zones;
-  for(uint32_t b = threadIdx.x; b < nz; b += kBlock) s_hist[b] = 0;
+  for(uint32_t b = threadIdx.x; b < nz; b += kLandThreads) s_hist[b] = 0;
   __syncthreads();
-  uint32_t zt = 0;
-  if(valid)
-  {
-    zt = rdiv(to) >> kZoneBits;
-    atomicAdd(&s_hist[zt], 1u);
-  }
-  __syncthreads();
-  for(uint32_t b = threadIdx.x; b < nz; b += kBlock)
-  {
-    if(s_hist[b]) s_base[b] = atomicAdd(&c_eng.land_n[cur][b], s_hist[b]);
-    s_hist[b] = 0;
-  }
-  __syncthreads();
-  if(valid)
-  {
-    const uint32_t pos = s_base[zt] + atomicAdd(&s_hist[zt], 1u);
-    if(pos < zone_capacity(zt))
+  uint32_t zt[kLandPer], rk[kLandPer];
+#pragma unroll
+  for(int u = 0; u < kLandPer; ++u)
+    if(r[u].valid)
     {
-      ZRec r;
-      r.w0 = w_noto | (rdiv(to) & kZoneMask);
-      r.from = from;
-      r.arg = arg;
-      *reinterpret_cast<uint4*>(c_eng.land[cur] + c_eng.zoff[zt] + pos) =
-        *reinterpret_cast<const uint4*>(&r);
+      zt[u] = rdiv(r[u].to) >> kZoneBits;
+      rk[u] = atomicAdd(&s_hist[zt[u]], 1u);
     }
-    else
-      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
-  }
+  __syncthreads();
+  for(uint32_t b = threadIdx.x; b < nz; b += kLandThreads)
+    if(s_hist[b]) s_base[b] = atomicAdd(&c_eng.land_n[cur][b], s_hist[b]);
+  __syncthreads();
+#pragma unroll
+  for(int u = 0; u < kLandPer; ++u)
+    if(r[u].valid)
+    {
+      const uint32_t pos = s_base[zt[u]] + rk[u];
+      if(pos < zone_capacity(zt[u]))
+      {
+        uint4 v;
+        v.x = r[u].w | (rdiv(r[u].to) & kZoneMask);
+        v.y = r[u].from;
+        v.z = (uint32_t)r[u].arg;
+        v.w = (uint32_t)(r[u].arg >> 32);
+        *reinterpret_cast<uint4*>(c_eng.land[cur] + c_eng.zoff[zt[u]] + pos) = v;
+      }
+      else
+        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    }
 }
 
 // Host sends (pony_sendv from outside the runtime): hseq gives the canonical
 // order; host senders rank above every actor id.
-__global__ void __launch_bounds__(kBlock) k_inject(const gpu_msg_t* msgs, uint64_t n,
+__global__ void __launch_bounds__(kLandThreads) k_inject(const gpu_msg_t* msgs, uint64_t n,
   uint64_t hseq_base, uint32_t cur)
 {
   __shared__ uint32_t s_hist[kMaxZones];
   __shared__ uint32_t s_base[kMaxZones];
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  bool valid = false;
-  uint32_t to = 0, w = 0, from = 0;
-  uint64_t arg = 0;
-  if(i < n)
+  LandRec r[kLandPer];
+#pragma unroll
+  for(int u = 0; u < kLandPer; ++u)
   {
-    const gpu_msg_t m = msgs[i];
-    const uint64_t hseq = hseq_base + i;
-    if(!is_remote(m.to))
+    const uint64_t i = (uint64_t)blockIdx.x * kLandRecs + (uint64_t)u * kLandThreads + threadIdx.x;
+    r[u].valid = false;
+    if(i < n)
     {
-      const int t = type_of_global(m.to);
-      if(t >= 0 && c_types[t].reducible)
+      const gpu_msg_t m = msgs[i];
+      const uint64_t hseq = hseq_base + i;
+      if(!is_remote(m.to))
       {
-        reducible_apply_local(m.to, m.behaviour, m.arg);
-        atomicAdd(&c_eng.stats[ST_DELIVERED], 1ull);
-        atomicAdd(&c_eng.stats[ST_BY_TYPE + t], 1ull);
-      }
-      else if(t >= 0)
-      {
-        valid = true;
-        to = m.to;
-        w = ((uint32_t)(hseq & 0xFFFFull) << 16) | ((m.behaviour & 0xFu) << 12);
-        from = kHostFrom | (uint32_t)(hseq >> 16);
-        arg = m.arg;
+        const int t = type_of_global(m.to);
+        if(t >= 0 && c_types[t].reducible)
+        {
+          reducible_apply_local(m.to, m.behaviour, m.arg);
+          atomicAdd(&c_eng.stats[ST_DELIVERED], 1ull);
+          atomicAdd(&c_eng.stats[ST_BY_TYPE + t], 1ull);
+        }
+        else if(t >= 0)
+        {
+          r[u].valid = true;
+          r[u].to = m.to;
+          r[u].w = ((uint32_t)(hseq & 0xFFFFull) << 16) | ((m.behaviour & 0xFu) << 12);
+          r[u].from = kHostFrom | (uint32_t)(hseq >> 16);
+          r[u].arg = m.arg;
+        }
       }
     }
   }
-  land_block(valid, to, w, from, arg, cur, s_hist, s_base);
+  land_records(r, cur, s_hist, s_base);
 }
 
 // Records received from other ranks.
-__global__ void __launch_bounds__(kBlock) k_xinject(const XRec* in, uint64_t n, uint32_t cur)
+__global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64_t n, uint32_t cur)
 {
   __shared__ uint32_t s_hist[kMaxZones];
   __shared__ uint32_t s_base[kMaxZones];
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  bool valid = false;
-  uint32_t to = 0, w = 0, from = 0;
-  uint64_t arg = 0;
   __shared__ unsigned long long s_app[GPU_ACTOR_MAX_TYPES];
   if(threadIdx.x < GPU_ACTOR_MAX_TYPES) s_app[threadIdx.x] = 0;
   __syncthreads();
-  if(i < n)
+  LandRec r[kLandPer];
+#pragma unroll
+  for(int u = 0; u < kLandPer; ++u)
   {
-    const XRec x = in[i];
-    if((x.w >> 16) == kSeqApply)
+    const uint64_t i = (uint64_t)blockIdx.x * kLandRecs + (uint64_t)u * kLandThreads + threadIdx.x;
+    r[u].valid = false;
+    if(i < n)
     {
-      reducible_apply_local(x.to, (x.w >> 12) & 0xFu, x.arg);
-      const int t = type_of_global(x.to);
-      if(t >= 0) atomicAdd(&s_app[t], 1ull);
-    }
-    else
-    {
-      valid = true;
-      to = x.to; w = x.w; from = x.from; arg = x.arg;
+      const XRec x = in[i];
+      if((x.w >> 16) == kSeqApply)
+      {
+        reducible_apply_local(x.to, (x.w >> 12) & 0xFu, x.arg);
+        const int t = type_of_global(x.to);
+        if(t >= 0) atomicAdd(&s_app[t], 1ull);
+      }
+      else
+      {
+        r[u].valid = true;
+        r[u].to = x.to; r[u].w = x.w; r[u].from = x.from; r[u].arg = x.arg;
+      }
     }
   }
-  land_block(valid, to, w, from, arg, cur, s_hist, s_base);
-  // land_block ends behind a barrier: s_app is complete
+  land_records(r, cur, s_hist, s_base);
+  // land_records passed barriers after every s_app update
   if(threadIdx.x < GPU_ACTOR_MAX_TYPES && s_app[threadIdx.x])
   {
     atomicAdd(&c_eng.stats[ST_DELIVERED], s_app[threadIdx.x]);
