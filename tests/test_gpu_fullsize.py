@@ -1,0 +1,101 @@
+"""GPU checks at BASELINE.json's full sizes.
+
+Where the CPU restatement finishes in seconds (message-ubench-det at 1M
+pingers, fan-in with 100K senders, gups on a 2^20 table) the engine is compared
+with it bit for bit. Where it does not (steady-state message-ubench at 1M
+pingers, the storm at 8M actors — one GPU's share of C5) the checks are the
+size-independent properties the workload has: message conservation, the sum of
+per-actor counts, and an XOR checksum of every payload delivered."""
+import numpy as np
+import pytest
+
+from ponyc_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+MILLION = 1 << 20
+
+
+def _same_as_oracle(engine_factory, oracle, setup, result):
+    e = engine_factory()
+    we = setup(e)
+    se = e.run()
+    ce = e.counts()
+    re = result(e, we)
+    wo = setup(oracle)
+    so = oracle.run()
+    co = oracle.counts()
+    ro = result(oracle, wo)
+    assert ce["dropped"] == 0
+    assert se == so
+    for k in ("delivered", "sent", "pending", "delivered_by_type"):
+        assert ce[k] == co[k], k
+    np.testing.assert_array_equal(re, ro)
+    return ce
+
+
+def test_c2_ubench_det_1m(engine_factory, oracle):
+    """C2, deterministic form: 1,048,576 pingers x 5 tokens x 4 hops."""
+    c = _same_as_oracle(engine_factory, oracle,
+                        lambda e: W.ubench(e, MILLION, 5, det=True, hops=3), W.ubench_result)
+    assert c["delivered"] == MILLION * 5 * 4
+
+
+def test_c2_ubench_steady_1m(engine_factory):
+    """C2 as benched: 1,048,576 pingers x 5 pings, no forward budget. Every
+    step delivers (and forwards) exactly the 5N pings in flight."""
+    n, initial, steps = MILLION, 5, 12
+    e = engine_factory()
+    w = W.ubench(e, n, initial, budget=1 << 62)
+    e.run_fixed(steps)
+    c = e.counts()
+    assert c["dropped"] == 0
+    assert c["delivered"] == steps * n * initial
+    assert c["sent"] == c["delivered"]
+    assert c["pending"] == n * initial
+    st = W.ubench_result(e, w)            # [x, y, count]
+    assert int(st[2].sum()) == c["delivered"]
+    # the xoroshiro128+ streams advanced once per ping handled
+    assert int(st[2].max()) < 20 * steps
+
+
+def test_c3_fanin_100k(engine_factory, oracle):
+    """C3: 100,000 senders -> 4 analyzers x 100 messages (atomic-enqueue
+    contention worst case; analyzer counts and XOR folds bit-exact)."""
+    c = _same_as_oracle(engine_factory, oracle,
+                        lambda e: W.fanin(e, 100_000, 4, 100, 0), W.fanin_result)
+    assert c["delivered_by_type"][0] == 100_000 * 100
+
+
+def test_c4_gups_2p20(engine_factory, oracle):
+    """C4 on one GPU: 2^20-entry table over 8 updaters, 4 streamers x 1024
+    updates x 1001 iterations."""
+    _same_as_oracle(engine_factory, oracle, lambda e: W.gups(e, 20, 8, 4, 1024, 1000),
+                    W.gups_result)
+
+
+def test_c5_storm_8m(engine_factory):
+    """C5, one GPU's share: 8M actors, a token ring plus 4 random-target pings
+    per actor, 4 hops each. Conservation and an XOR checksum of every payload."""
+    n, r, hops = 8 * MILLION, 4, 4
+    e = engine_factory()
+    w = W.storm(e, n, r, hops)
+    e.run()
+    c = e.counts()
+    assert c["dropped"] == 0 and c["pending"] == 0
+    total = n * (r + 1) * (hops + 1)
+    assert c["delivered"] == total
+    st = e.state_read(w["type"])          # [count, acc]
+    assert int(st[0].sum()) == total
+    # tokens: every actor sees hop values 0..hops once
+    tok = 0
+    for h in range(hops + 1):
+        tok ^= h
+    tok_all = tok if n % 2 else 0
+    # pings: origin o in [0, n*r) carries (o << 32) | h for h = 0..hops
+    o = np.arange(n * r, dtype=np.uint64)
+    ox = int(np.bitwise_xor.reduce(o << np.uint64(32)))
+    ping_all = 0
+    for h in range(hops + 1):
+        ping_all ^= ox ^ (h if (n * r) % 2 else 0)
+    assert int(np.bitwise_xor.reduce(st[1])) == tok_all ^ ping_all
