@@ -38,10 +38,14 @@ constexpr uint32_t kIdxCap = 16384;   // LDS index budget per zone (records per 
 constexpr uint32_t kTile = 4096;      // outbox records sorted per scatter tile (64 KB of LDS)
 constexpr int kTilePer = kTile / 512; // tile records per thread
 constexpr int kIdxPer = kIdxCap / 512; // landed records per thread on the LDS-index path
-#ifndef GPA_SMALL
-#define GPA_SMALL 16
-#endif
-constexpr uint32_t kSmall = GPA_SMALL;  // arrival groups up to this size are ordered in registers
+// Arrival groups up to this size are loaded at once and ordered in registers.
+// 16 where the handler does not read the message (pinger: the selection
+// compiles away) or the table's state is small; 8 elsewhere, to stay within
+// 128 VGPRs without spilling.
+template <int HT> __host__ __device__ constexpr uint32_t small_regs()
+{
+  return (HT == GPU_ACTOR_HT_PINGER || HT == GPU_ACTOR_HT_FANIN_SENDER) ? 16u : 8u;
+}
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
@@ -213,22 +217,23 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
   for(int k = 0; k < NW; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
   const uint32_t g = n - nc;
   const uint32_t hc = min(w, nc);                 // carried messages handled now
-  const bool small = g > 0 && w - hc >= g && g <= kSmall;
+  constexpr uint32_t SM = small_regs<HT>();
+  const bool small = g > 0 && w - hc >= g && g <= SM;
   // small arrival group: its records are loaded with the state, before any
-  // handler runs (one round of memory latency for the actor)
-  uint64_t k[kSmall], v[kSmall];
-  uint32_t bh[kSmall];
+  // handler runs (one round of memory latency for the actor); the behaviour
+  // rides in the key's low bits (key << 4 | beh sorts like the key)
+  uint64_t k[SM], v[SM];
 #pragma unroll
-  for(int j = 0; j < (int)kSmall; ++j)
+  for(int j = 0; j < (int)SM; ++j)
   {
     if(small && (uint32_t)j < g)
     {
       const ZRec r = acc.rec(nc + j);
-      k[j] = zkey(r); v[j] = r.arg; bh[j] = (r.w0 >> 12) & 0xFu;
+      k[j] = (zkey(r) << 4) | ((r.w0 >> 12) & 0xFu); v[j] = r.arg;
     }
     else
     {
-      k[j] = ~0ull; v[j] = 0; bh[j] = 0;
+      k[j] = ~0ull; v[j] = 0;
     }
   }
   // Wait for those loads here, once: otherwise the wait lands at the head of
@@ -242,38 +247,23 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
     handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
     ++done;
   }
-  bool sorted_tail = true;
   if(g > 0)
   {
     const uint32_t q = w - done;
     if(small)
     {
       // small group handled whole: all records in registers, select by key
-      bool g_done = false;
-#ifdef GPA_SAME_SMALL
-      // A handler sees only (behaviour, arg): when every record of the group
-      // carries the same pair, any order of them is the canonical one.
-      bool same = true;
-#pragma unroll
-      for(int j = 1; j < (int)kSmall; ++j)
-        if((uint32_t)j < g) same = same && v[j] == v[0] && bh[j] == bh[0];
-      if(same)
-      {
-        for(uint32_t r = 0; r < g; ++r) handle<HT>(T, a, s, bh[0], v[0], nullptr);
-        g_done = true;
-      }
-#endif
-      for(uint32_t r = 0; r < g && !g_done; ++r)
+      for(uint32_t r = 0; r < g; ++r)
       {
         uint64_t best = k[0], barg = v[0];
-        uint32_t bb = bh[0], bi = 0;
+        uint32_t bi = 0;
 #pragma unroll
-        for(int j = 1; j < (int)kSmall; ++j)
-          if(k[j] < best) { best = k[j]; barg = v[j]; bb = bh[j]; bi = (uint32_t)j; }
+        for(int j = 1; j < (int)SM; ++j)
+          if(k[j] < best) { best = k[j]; barg = v[j]; bi = (uint32_t)j; }
 #pragma unroll
-        for(int j = 0; j < (int)kSmall; ++j)
+        for(int j = 0; j < (int)SM; ++j)
           if((uint32_t)j == bi) k[j] = ~0ull;
-        handle<HT>(T, a, s, bb, barg, nullptr);
+        handle<HT>(T, a, s, (uint32_t)best & 0xFu, barg, nullptr);
       }
       done += g;
     }
@@ -281,22 +271,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
     {
       // large group handled whole: select in key order
       uint64_t last = 0;
-      bool same = false;
-#ifdef GPA_SAME_LARGE
-      {
-        const ZRec r0 = acc.rec(nc);
-        const uint32_t w0 = r0.w0 & 0xF000u;
-        same = true;
-        for(uint32_t j = 1; j < g && same; ++j)
-        {
-          const ZRec rj = acc.rec(nc + j);
-          same = rj.arg == r0.arg && (rj.w0 & 0xF000u) == w0;
-        }
-        if(same)
-          for(uint32_t r = 0; r < g; ++r) handle<HT>(T, a, s, w0 >> 12, r0.arg, nullptr);
-      }
-#endif
-      for(uint32_t r = 0; r < g && !same; ++r)
+      for(uint32_t r = 0; r < g; ++r)
       {
         uint64_t best = ~0ull;
         uint32_t bi = 0;
@@ -323,7 +298,6 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
       done += q;
     }
   }
-  (void)sorted_tail;
 #pragma unroll
   for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
   // the unhandled tail, canonical, becomes next step's carried mail

@@ -7,9 +7,6 @@ b() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -
 for v in "$@"; do
   case $v in
     base) b base ;;
-    ssmall) b ssmall -DGPA_SAME_SMALL ;;
-    r8) b r8 -DGPA_SMALL=8 ;;
-    r16) b r16 -DGPA_SMALL=16 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
