@@ -33,6 +33,7 @@ constexpr uint32_t kMaxRanks = 64;
 constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above every actor
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
 constexpr uint32_t kSeqApply = 0xFFFFu;          // outbox marker: reducible apply
+constexpr uint32_t kFanLds = 256;                // analyzers a zone accumulates in LDS
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
@@ -157,6 +158,13 @@ struct ActorCtx {
   uint32_t* s_nout;      // LDS outbox counter
   uint32_t* s_hist;      // LDS histogram by bucket
   unsigned long long* agg;   // this wave's LDS aggregation word
+  unsigned long long* fan;   // zone accumulators of fan-in applies (LDS, 2 x kFanLds) or null
+  int      fan_t;        // analyzer type those accumulators are for
+  // the reducible type last applied to (gups updater), cached so that a run
+  // of applies does not look the type up, and wait, once per message
+  uint32_t rc_first, rc_count, rc_lfirst, rc_lcount;
+  uint64_t* rc_state;
+  uint64_t rc_mask;
 };
 
 // ---- delivery --------------------------------------------------------------
@@ -290,10 +298,19 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
       {
         const TypeDev& T = c_types[t];
         const uint32_t li = rdiv(tl) - T.lfirst;
-        atomicAdd(reinterpret_cast<unsigned long long*>(&T.state[li]),
-          (unsigned long long)__popcll(peers));
-        atomicXor(reinterpret_cast<unsigned long long*>(&T.state[(size_t)T.lcount + li]),
-          *agg);
+        if(a.fan && t == a.fan_t && li < kFanLds)
+        {
+          // zone accumulator: one global atomic per (zone, analyzer) at the end
+          atomicAdd(&a.fan[li], (unsigned long long)__popcll(peers));
+          atomicXor(&a.fan[kFanLds + li], *agg);
+        }
+        else
+        {
+          atomicAdd(reinterpret_cast<unsigned long long*>(&T.state[li]),
+            (unsigned long long)__popcll(peers));
+          atomicXor(reinterpret_cast<unsigned long long*>(&T.state[(size_t)T.lcount + li]),
+            *agg);
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -310,8 +327,21 @@ __device__ __forceinline__ void send_updater(ActorCtx& a, uint32_t to, uint64_t 
     return;
   }
   a.applied++;
-  if(a.applied_type < 0) a.applied_type = type_of_global(to);
-  reducible_apply_local(to, GPU_ACTOR_GUPS_UPDATE, d);
+  if(to - a.rc_first >= a.rc_count)
+  {
+    const int t = type_of_global(to);
+    if(t < 0) return;
+    const TypeDev& T = c_types[t];
+    if(a.applied_type < 0) a.applied_type = t;
+    a.rc_first = T.first; a.rc_count = T.count;
+    a.rc_lfirst = T.lfirst; a.rc_lcount = T.lcount;
+    a.rc_state = T.state;
+    a.rc_mask = T.params[0] - 1;
+  }
+  // gups_basic Updater.apply: t[d & (size - 1)] ^= d
+  const uint32_t li = rdiv(to) - a.rc_lfirst;
+  atomicXor(reinterpret_cast<unsigned long long*>(&a.rc_state[(d & a.rc_mask) * a.rc_lcount + li]),
+    (unsigned long long)d);
 }
 
 // ---- handler tables --------------------------------------------------------

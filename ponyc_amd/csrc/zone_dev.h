@@ -338,9 +338,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
+  constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
+  __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
   const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
+  if constexpr(kFan)
+    for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
   const uint32_t nxt = cur ^ 1u;
   const uint32_t L0 = z * kZone;
   const uint32_t nact = min(kZone, c_eng.n_local - L0);
@@ -509,6 +513,18 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   a.nxt = nxt;
   a.s_hist = s_hist;
   a.agg = &s_agg[wv];
+  // fan-in senders fold their analyzer applies per zone in LDS
+  a.fan = nullptr;
+  a.fan_t = -1;
+  a.rc_first = a.rc_count = a.rc_lfirst = a.rc_lcount = 0;
+  a.rc_state = nullptr;
+  a.rc_mask = 0;
+  if constexpr(kFan)
+    if(tz >= 0 && c_types[tz].ht == GPU_ACTOR_HT_FANIN_SENDER)
+    {
+      a.fan_t = type_of_global((uint32_t)c_types[tz].params[1]);
+      if(a.fan_t >= 0) a.fan = s_fan;
+    }
   ZRec* Cout = c_eng.carry[nxt] + c_eng.zoff[z];
   uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
   // drain local actor i, of type t (T = c_types[t])
@@ -584,6 +600,18 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(4);
   if(tid < GPU_ACTOR_MAX_TYPES && s_bytype[tid])
     atomicAdd(&c_eng.stats[ST_BY_TYPE + tid], s_bytype[tid]);
+  if constexpr(kFan)
+    if(a.fan)
+    {
+      const TypeDev& F = c_types[a.fan_t];
+      for(uint32_t j = tid; j < kFanLds && j < F.lcount; j += kZoneThreads)
+        if(s_fan[j])
+        {
+          atomicAdd(reinterpret_cast<unsigned long long*>(&F.state[j]), s_fan[j]);
+          atomicXor(reinterpret_cast<unsigned long long*>(&F.state[(size_t)F.lcount + j]),
+            s_fan[kFanLds + j]);
+        }
+    }
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
