@@ -1,7 +1,7 @@
 // engine.hip — the gpu_actor engine for gfx950: kernels (zone_dev.h) and the
 // C-ABI declared in include/gpu_actor.h.
 //
-// One superstep = one k_step launch (one workgroup per 4096-actor zone; see
+// One superstep = one k_step launch (one workgroup per 2048-actor zone; see
 // zone_dev.h). With n_ranks > 1, the records a step produced for actors on
 // other ranks are swapped with RCCL after it (counts all-to-all, then grouped
 // ncclSend/ncclRecv over xGMI) and k_xinject lands them before the next step.

@@ -2,7 +2,7 @@
 // tables of the gpu_actor engine. See DESIGN.md for the rationale.
 //
 // HBM layout (per rank; actor id a lives on rank a % R at local slot L = a / R):
-//   Local slots are cut into zones of kZone (4096) actors. Zone z owns
+//   Local slots are cut into zones of kZone (2048) actors. Zone z owns
 //     land[p][z]   : landing buffer of step-p arrivals (unordered 16-B ZRecs),
 //                    filled by producers in chunks, one atomicAdd on
 //                    land_n[p][z] per (producer zone, destination zone);

@@ -1,21 +1,25 @@
 // zone_dev.h — the superstep kernel (k_step) and the injection kernels.
 //
-// k_step runs one 1024-thread workgroup per zone of 4096 actors and replaces,
+// k_step runs one 512-thread workgroup per zone of 2048 actors and replaces,
 // for those actors, ponyint_actor_run's pop loop (actor.c:383-549), the MPSC
 // push/pop (messageq.c:31-59,234-258) and the scheduler's run/steal loop
 // (scheduler.c:752-1090):
 //   1. count the zone's carried and newly landed records per actor (LDS
-//      atomics) and scan them into per-actor segments;
-//   2. place them into the zone's sorted-inbox scratch S (carry first, in
-//      canonical order; new arrivals after, in landing order);
+//      atomics; each landed record's rank comes back from its atomic) and
+//      scan them into per-actor segments;
+//   2. place an LDS index (u16) of every record at its segment position
+//      (carry first, canonical; new arrivals after, in landing order) — or,
+//      for a zone with more records than the index holds, the records
+//      themselves into the scratch S;
 //   3. per actor: handle min(batch, n) messages — carried mail, then the new
 //      group in (from, seq) key order — with the actor's state in registers;
 //      sends are parked in the zone outbox O and counted per destination
 //      bucket (zone, or peer rank) in LDS; the unhandled tail is written to
 //      the zone's carry buffer for the next step, already canonical;
 //   4. reserve one contiguous chunk per destination bucket with ONE
-//      atomicAdd per (zone, bucket) and scatter the outbox into the
-//      destination zones' landing buffers (or the per-peer exchange buffer).
+//      atomicAdd per (zone, bucket) and scatter the outbox, sorted by bucket
+//      in LDS tiles, into the destination zones' landing buffers (or the
+//      per-peer exchange buffer).
 // Workgroups never wait on each other: all inter-zone traffic goes through
 // the next launch (the step boundary is the BSP barrier).
 #pragma once
