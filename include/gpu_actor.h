@@ -125,6 +125,16 @@ GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t 
 /* Bulk-create `count` actors of a type (once per type); ids are
  * [*first_id, *first_id + count). Runs the table's constructor on device. */
 GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* first_id);
+/* Room for `n` more actors of a type that behaviours create while running
+ * (pony_create inside a behaviour + its constructor message, actor.c:688-734,
+ * gencall.c:606-612). Call before gpu_actor_create; the type's id range
+ * becomes [first, first + count + n). A spawned actor's id is assigned at the
+ * end of the superstep that created it, in (creator id, creator send
+ * sequence) order after the type's live actors; its constructor message is
+ * delivered in the next superstep like any other send. Single rank only. */
+GPU_ACTOR_API int gpu_actor_type_reserve(uint32_t type_id, uint64_t n);
+/* Live (created + spawned) actors of a type. */
+GPU_ACTOR_API int gpu_actor_type_live(uint32_t type_id, uint64_t* live);
 
 /* ---- sending from the host (pony_alloc_msg + pony_sendv, actor.c:749-817) */
 /* Host staging buffer for up to n messages, owned by the library and valid
@@ -253,6 +263,20 @@ GPU_ACTOR_API const char* gpu_actor_strerror(int code);
 #define GPU_ACTOR_FIFO_BURST         0
 #define GPU_ACTOR_HT_FIFO_SINK       10
 #define GPU_ACTOR_FIFO_PUSH          0
+
+/* Spreader (examples/spreader/main.pony:1-48): builds a binary tree of
+ * 2^count - 1 actors by spawning, then sums the node counts back up.
+ *   state: [0] count [1] parent id (~0 = none: the root)
+ *          [2] _result [3] _received [4] root's printed total (result + 1)
+ *   behaviours: SPREAD(parent << 32 | count) — the constructor
+ *               (new create / new spread): if count == 1: RESULT(1) to parent
+ *               (the root sets [4] = 1) else spawn two Spreaders with
+ *               SPREAD(self << 32 | count - 1);
+ *               RESULT(i): received++, result += i; at 2: RESULT(result + 1)
+ *               to parent, or the root sets [4] = result + 1                */
+#define GPU_ACTOR_HT_SPREADER        11
+#define GPU_ACTOR_SPREADER_SPREAD    0
+#define GPU_ACTOR_SPREADER_RESULT    1
 
 #define GPU_ACTOR_NONE 0xFFFFFFFFFFFFFFFFULL
 

@@ -40,10 +40,15 @@ typedef struct {
   int      registered, created;
   uint32_t words, ht, batch, cap, reducible;
   uint64_t params[GPU_ACTOR_MAX_PARAMS];
-  uint64_t first, count;
+  uint64_t first, count;  /* id range [first, first + count): created + reserve */
+  uint64_t live;          /* created + spawned so far                        */
+  uint64_t reserve;       /* room for actors spawned by behaviours           */
   uint64_t* state;        /* field-major: state[w * count + i] */
   uint64_t delivered;
 } otype_t;
+
+/* an actor created by a behaviour this step: id assigned at the step's end */
+typedef struct { uint32_t type, beh; uint64_t arg; } ospawn_t;
 
 static struct {
   int       init;
@@ -52,6 +57,8 @@ static struct {
   uint8_t*  type_of;      /* actor id -> type id */
   mbox_t*   mb;
   uint64_t  steps, delivered, sent, dropped;
+  ospawn_t* spawns;       /* this step's, in (creator id, call order) order */
+  uint64_t  n_spawns, spawns_alloc;
 } S;
 
 static const uint32_t DEFAULT_BATCH = 100;   /* PONY_SCHED_BATCH, actor.c:20 */
@@ -79,12 +86,28 @@ void or_shutdown(void)
     free(S.mb[a].buf);
   free(S.mb);
   free(S.type_of);
+  free(S.spawns);
   memset(&S, 0, sizeof(S));
+}
+
+int or_type_reserve(uint32_t type_id, uint64_t n)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered ||
+    S.types[type_id].created) return GPU_ACTOR_EINVAL;
+  S.types[type_id].reserve = n;
+  return 0;
+}
+
+int or_type_live(uint32_t type_id, uint64_t* out)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].created) return GPU_ACTOR_EINVAL;
+  *out = S.types[type_id].live;
+  return 0;
 }
 
 int or_type_register(uint32_t type_id, uint32_t state_words, uint32_t ht)
 {
-  if(!S.init || type_id >= GPU_ACTOR_MAX_TYPES || ht < 1 || ht > 10) return GPU_ACTOR_EINVAL;
+  if(!S.init || type_id >= GPU_ACTOR_MAX_TYPES || ht < 1 || ht > 11) return GPU_ACTOR_EINVAL;
   otype_t* t = &S.types[type_id];
   if(t->registered) return GPU_ACTOR_EINVAL;
   t->registered = 1;
@@ -118,7 +141,7 @@ static void construct(uint32_t tid)
   otype_t* t = &S.types[tid];
   uint64_t n = t->count;
   uint64_t* st = t->state;
-  for(uint64_t i = 0; i < n; i++)
+  for(uint64_t i = 0; i < t->live; i++)    /* reserved actors start zeroed */
   {
     switch(t->ht)
     {
@@ -180,6 +203,8 @@ int or_create(uint32_t type_id, uint64_t count, uint64_t* first_id)
   if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
   otype_t* t = &S.types[type_id];
   if(!t->registered || t->created) return GPU_ACTOR_EINVAL;
+  const uint64_t live = count;
+  count += t->reserve;
   uint64_t total = S.n_actors + count;
   uint8_t* to = realloc(S.type_of, total ? total : 1);
   mbox_t* mb = realloc(S.mb, (total ? total : 1) * sizeof(mbox_t));
@@ -192,6 +217,7 @@ int or_create(uint32_t type_id, uint64_t count, uint64_t* first_id)
   }
   t->first = S.n_actors;
   t->count = count;
+  t->live = live;
   t->state = calloc(t->words * count + 1, sizeof(uint64_t));
   if(!t->state) return GPU_ACTOR_ENOMEM;
   t->created = 1;
@@ -274,6 +300,43 @@ int or_sendv(const void* msgs, uint64_t n)
     if(rc) return rc;
   }
   return 0;
+}
+
+/* pony_create inside a behaviour + the constructor message (actor.c:688-734,
+ * gencall.c:606-612): the new actor's id is assigned when the step ends. */
+static void spawn(uint32_t type, uint32_t beh, uint64_t arg)
+{
+  S.sent++;
+  if(S.n_spawns == S.spawns_alloc)
+  {
+    uint64_t nc = S.spawns_alloc ? 2 * S.spawns_alloc : 64;
+    ospawn_t* nb = realloc(S.spawns, nc * sizeof(ospawn_t));
+    if(!nb) { S.dropped++; return; }
+    S.spawns = nb;
+    S.spawns_alloc = nc;
+  }
+  S.spawns[S.n_spawns].type = type;
+  S.spawns[S.n_spawns].beh = beh;
+  S.spawns[S.n_spawns].arg = arg;
+  S.n_spawns++;
+}
+
+/* End of a step: spawned actors get ids per type in (creator id, call order)
+ * order — the order they were recorded in, actors being visited by id — and
+ * their constructor messages are appended to their (empty) mailboxes. */
+static void place_spawns(void)
+{
+  for(uint32_t ty = 0; ty < GPU_ACTOR_MAX_TYPES; ty++)
+    for(uint64_t k = 0; k < S.n_spawns; k++)
+    {
+      if(S.spawns[k].type != ty) continue;
+      otype_t* t = &S.types[ty];
+      if(t->live >= t->count) { S.dropped++; continue; }
+      const uint64_t id = t->first + t->live;
+      t->live++;
+      deliver(id, S.spawns[k].beh, S.spawns[k].arg);
+    }
+  S.n_spawns = 0;
 }
 
 /* ---- behaviours ---------------------------------------------------------- */
@@ -379,6 +442,38 @@ static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
       break;
     }
 
+    case GPU_ACTOR_HT_SPREADER:
+      if(beh == GPU_ACTOR_SPREADER_SPREAD)
+      {
+        /* new create / new spread (spreader/main.pony:9-32) */
+        const uint64_t parent = arg >> 32, count = arg & 0xFFFFFFFFULL;
+        W(0) = count;
+        W(1) = parent == 0xFFFFFFFFULL ? GPU_ACTOR_NONE : parent;
+        if(count <= 1)
+        {
+          if(W(1) != GPU_ACTOR_NONE) send(W(1), GPU_ACTOR_SPREADER_RESULT, 1);
+          else W(4) = 1;                           /* env.out.print("1 actor") */
+        }
+        else
+        {
+          /* spawn_child() x 2 (spreader/main.pony:47-48) */
+          spawn(S.type_of[self], GPU_ACTOR_SPREADER_SPREAD, (self << 32) | (count - 1));
+          spawn(S.type_of[self], GPU_ACTOR_SPREADER_SPREAD, (self << 32) | (count - 1));
+        }
+      }
+      else
+      {
+        /* be result(i) (spreader/main.pony:34-45) */
+        W(3) += 1;
+        W(2) += arg;
+        if(W(3) == 2)
+        {
+          if(W(1) != GPU_ACTOR_NONE) send(W(1), GPU_ACTOR_SPREADER_RESULT, W(2) + 1);
+          else W(4) = W(2) + 1;                    /* print(_result + 1 " actors") */
+        }
+      }
+      break;
+
     case GPU_ACTOR_HT_FIFO_SINK: {
       uint64_t ns = t->params[0] ? t->params[0] : 1;
       uint64_t slot = ((arg >> 32) / ns) % 8;
@@ -430,6 +525,7 @@ int or_run(uint64_t max_steps, uint64_t* steps_done)
         handle(t, a, r.beh, r.arg);
       }
     }
+    place_spawns();
     /* the window for host sends after this step starts at the new head */
     for(uint64_t a = 0; a < S.n_actors; a++)
       S.mb[a].head_start = S.mb[a].head;

@@ -59,6 +59,9 @@ int  or_type_register(uint32_t type_id, uint32_t state_words, uint32_t ht);
 int  or_type_config(uint32_t type_id, uint32_t batch, uint32_t mailbox_cap);
 int  or_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
 int  or_create(uint32_t type_id, uint64_t count, uint64_t* first_id);
+/* room for n actors created by behaviours (before or_create); live count */
+int  or_type_reserve(uint32_t type_id, uint64_t n);
+int  or_type_live(uint32_t type_id, uint64_t* out);
 int  or_send(uint64_t to, uint32_t behaviour, uint64_t arg);
 int  or_sendv(const void* msgs, uint64_t n);   /* msgs: gpu_msg_t[n] */
 int  or_run(uint64_t max_steps, uint64_t* steps_done);

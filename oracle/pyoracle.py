@@ -47,6 +47,8 @@ def load():
         "or_type_config": (i32, [u32, u32, u32]),
         "or_type_param": (i32, [u32, u32, u64]),
         "or_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
+        "or_type_reserve": (i32, [u32, u64]),
+        "or_type_live": (i32, [u32, ctypes.POINTER(u64)]),
         "or_send": (i32, [u64, u32, u64]), "or_sendv": (i32, [vp, u64]),
         "or_run": (i32, [u64, ctypes.POINTER(u64)]),
         "or_state_read": (i32, [u32, u64, u64, vp]),
@@ -86,6 +88,7 @@ class Oracle:
         _ck("or_init", self.lib.or_init(16))
         self.n_ranks, self.rank = 1, 0
         self.words, self.first, self.count = {}, {}, {}
+        self.reserve = {}
         self.alive = True
 
     def type_register(self, type_id, state_words, ht):
@@ -98,10 +101,20 @@ class Oracle:
     def type_param(self, type_id, idx, value):
         _ck("or_type_param", self.lib.or_type_param(type_id, idx, int(value) & U64))
 
+    def type_reserve(self, type_id, n):
+        _ck("or_type_reserve", self.lib.or_type_reserve(type_id, n))
+        self.reserve[type_id] = n
+
+    def type_live(self, type_id):
+        v = ctypes.c_uint64(0)
+        _ck("or_type_live", self.lib.or_type_live(type_id, ctypes.byref(v)))
+        return v.value
+
     def create(self, type_id, count):
         first = ctypes.c_uint64(0)
         _ck("or_create", self.lib.or_create(type_id, count, ctypes.byref(first)))
-        self.first[type_id], self.count[type_id] = first.value, count
+        self.first[type_id] = first.value
+        self.count[type_id] = count + self.reserve.get(type_id, 0)
         return first.value
 
     def sendv(self, msgs):

@@ -8,6 +8,7 @@
 // The launch boundary is the BSP barrier; quiescence ("no pending mail on any
 // rank") replaces the CNF/ACK protocol (scheduler.c:303-480).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -23,11 +24,11 @@
 using namespace gpa;
 
 // pony_create's constructor run: initial state of a freshly created type.
-__global__ void __launch_bounds__(kBlock) k_construct(uint32_t t)
+__global__ void __launch_bounds__(kBlock) k_construct(uint32_t t, uint32_t n_live)
 {
   const TypeDev& T = c_types[t];
   const uint32_t li = blockIdx.x * kBlock + threadIdx.x;
-  if(li >= T.lcount) return;
+  if(li >= n_live) return;      // reserved (not yet spawned) actors stay zeroed
   const uint32_t L = T.lfirst + li;
   const uint64_t i = (uint64_t)L * c_eng.nranks + c_eng.rank - T.first;   // index in type
   const size_t n = T.lcount;
@@ -86,6 +87,60 @@ __global__ void __launch_bounds__(kBlock) k_zone_copy(const ZRec* src, const uin
   for(uint32_t i = threadIdx.x; i < src_cap[z]; i += kBlock) d[i] = s[i];
 }
 
+// ---- actors spawned by behaviours (gpu_actor_type_reserve) -------------------
+// After a step: the spawn records, sorted by key (type, creator, seq), get ids
+// first + live[type] + (rank within the type); each new actor's constructor
+// message lands like any other arrival for the next step.
+__global__ void __launch_bounds__(kBlock) k_spawn_scan(const uint64_t* key, uint32_t n,
+  uint32_t* tstart, uint32_t* tcnt)
+{
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if(i >= n) return;
+  const uint32_t t = (uint32_t)(key[i] >> 52);
+  atomicMin(&tstart[t], i);
+  atomicAdd(&tcnt[t], 1u);
+}
+
+__global__ void __launch_bounds__(kLandThreads) k_spawn_land(const uint64_t* key, const uint64_t* arg,
+  uint32_t n, const uint32_t* tstart, const unsigned long long* live, uint32_t cur)
+{
+  __shared__ uint32_t s_hist[kMaxZones];
+  __shared__ uint32_t s_base[kMaxZones];
+  LandRec r[kLandPer];
+#pragma unroll
+  for(int u = 0; u < kLandPer; ++u)
+  {
+    const uint64_t i = (uint64_t)blockIdx.x * kLandRecs + (uint64_t)u * kLandThreads + threadIdx.x;
+    r[u].valid = false;
+    if(i < n)
+    {
+      const uint64_t k = key[i];
+      const uint32_t t = (uint32_t)(k >> 52);
+      const TypeDev& T = c_types[t];
+      const uint64_t slot = live[t] + (i - tstart[t]);
+      if(slot < T.count)
+      {
+        r[u].valid = true;
+        r[u].to = T.first + (uint32_t)slot;
+        r[u].w = (uint32_t)(((k >> 4) & 0xFFFFull) << 16) | (uint32_t)((k & 0xFu) << 12);
+        r[u].from = (uint32_t)(k >> 20);
+        r[u].arg = arg[i];
+      }
+      else
+        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    }
+  }
+  land_records(r, cur, s_hist, s_base);
+}
+
+__global__ void k_spawn_commit(const uint32_t* tcnt, unsigned long long* live)
+{
+  const uint32_t t = threadIdx.x;
+  if(t >= GPU_ACTOR_MAX_TYPES || tcnt[t] == 0) return;
+  const unsigned long long room = c_types[t].count - live[t];
+  live[t] += tcnt[t] < room ? tcnt[t] : room;
+}
+
 // ===========================================================================
 // Host side
 // ===========================================================================
@@ -102,6 +157,7 @@ struct HostType {
   uint64_t params[GPU_ACTOR_MAX_PARAMS] = {};
   uint64_t first = 0, count = 0;
   uint32_t lfirst = 0, lcount = 0;
+  uint64_t reserve = 0;                 // ids for actors spawned by behaviours
   uint64_t* d_state = nullptr;
 };
 
@@ -153,6 +209,14 @@ struct Engine {
   void* xp_ctx = nullptr;
   XRec* h_xout = nullptr;
   XRec* h_xin = nullptr;
+  // spawned actors (gpu_actor_type_reserve)
+  uint32_t spawn_cap = 0;
+  uint64_t *d_skey[2] = {nullptr, nullptr}, *d_sarg[2] = {nullptr, nullptr};
+  unsigned int* d_spawn_n = nullptr;
+  uint32_t *d_tstart = nullptr, *d_tcnt = nullptr;
+  unsigned long long* d_live = nullptr;  // [GPU_ACTOR_MAX_TYPES] live actors per type
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
 };
 
 Engine g;
@@ -226,6 +290,8 @@ int upload_types()
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
   e.dbg = g.d_dbg;
+  e.spawn_key = g.d_skey[0]; e.spawn_arg = g.d_sarg[0];
+  e.spawn_n = g.d_spawn_n; e.spawn_cap = g.spawn_cap;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   return 0;
@@ -323,6 +389,7 @@ uint32_t required_words(uint32_t ht)
     case GPU_ACTOR_HT_STORM: return 2;
     case GPU_ACTOR_HT_FIFO_SRC: return 3;
     case GPU_ACTOR_HT_FIFO_SINK: return 11;
+    case GPU_ACTOR_HT_SPREADER: return 5;
     default: return 0;
   }
 }
@@ -441,8 +508,45 @@ step_kernel_t pick_step_kernel()
     case GPU_ACTOR_HT_FANIN_SENDER: return k_step<GPU_ACTOR_HT_FANIN_SENDER>;
     case GPU_ACTOR_HT_GUPS_STREAMER: return k_step<GPU_ACTOR_HT_GUPS_STREAMER>;
     case GPU_ACTOR_HT_STORM: return k_step<GPU_ACTOR_HT_STORM>;
+    case GPU_ACTOR_HT_SPREADER: return k_step<GPU_ACTOR_HT_SPREADER>;
     default: return k_step<-1>;
   }
+}
+
+// Ids and landing for the actors the last step's behaviours created: the
+// records are sorted by (type, creator, seq) — the canonical order — and
+// numbered after each type's live actors (k_spawn_*). One small readback per
+// step, only for engines with a reserve.
+int spawn_process(uint32_t cur)
+{
+  unsigned int n = 0;
+  HIPCK(hipMemcpyAsync(&n, g.d_spawn_n, sizeof(n), hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  if(n == 0) return 0;
+  n = std::min(n, g.spawn_cap);
+  size_t need = 0;
+  HIPCK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, g.d_skey[0], g.d_skey[1], g.d_sarg[0],
+    g.d_sarg[1], (int)n, 0, 56, g.stream));
+  if(need > g.sort_tmp_bytes)
+  {
+    if(g.d_sort_tmp) HIPCK(hipFree(g.d_sort_tmp));
+    HIPCK(hipMalloc(&g.d_sort_tmp, need));
+    g.sort_tmp_bytes = need;
+  }
+  HIPCK(hipcub::DeviceRadixSort::SortPairs(g.d_sort_tmp, need, g.d_skey[0], g.d_skey[1],
+    g.d_sarg[0], g.d_sarg[1], (int)n, 0, 56, g.stream));
+  HIPCK(hipMemsetAsync(g.d_tstart, 0xFF, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t), g.stream));
+  HIPCK(hipMemsetAsync(g.d_tcnt, 0, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t), g.stream));
+  hipLaunchKernelGGL(k_spawn_scan, dim3(blocks_for(n)), dim3(kBlock), 0, g.stream,
+    (const uint64_t*)g.d_skey[1], n, g.d_tstart, g.d_tcnt);
+  hipLaunchKernelGGL(k_spawn_land, dim3(blocks_for(n, kLandRecs)), dim3(kLandThreads), 0, g.stream,
+    (const uint64_t*)g.d_skey[1], (const uint64_t*)g.d_sarg[1], n, (const uint32_t*)g.d_tstart,
+    (const unsigned long long*)g.d_live, cur);
+  hipLaunchKernelGGL(k_spawn_commit, dim3(1), dim3(64), 0, g.stream,
+    (const uint32_t*)g.d_tcnt, g.d_live);
+  HIPCK(hipGetLastError());
+  HIPCK(hipMemsetAsync(g.d_spawn_n, 0, sizeof(unsigned int), g.stream));
+  return 0;
 }
 
 // One superstep: k_step on parity g.par (+ exchange), then flip parity.
@@ -459,6 +563,11 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   if(R() > 1)
   {
     int rc = exchange(g.par);
+    if(rc) return rc;
+  }
+  if(g.spawn_cap)
+  {
+    int rc = spawn_process(g.par);
     if(rc) return rc;
   }
   return 0;
@@ -515,6 +624,16 @@ void free_all()
   if(g.d_O) (void)hipFree(g.d_O);
   if(g.d_zoff) (void)hipFree(g.d_zoff);
   if(g.d_zcap) (void)hipFree(g.d_zcap);
+  for(int p = 0; p < 2; ++p)
+  {
+    if(g.d_skey[p]) (void)hipFree(g.d_skey[p]);
+    if(g.d_sarg[p]) (void)hipFree(g.d_sarg[p]);
+  }
+  if(g.d_spawn_n) (void)hipFree(g.d_spawn_n);
+  if(g.d_tstart) (void)hipFree(g.d_tstart);
+  if(g.d_tcnt) (void)hipFree(g.d_tcnt);
+  if(g.d_live) (void)hipFree(g.d_live);
+  if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
   if(g.d_dbg) (void)hipFree(g.d_dbg);
@@ -617,6 +736,12 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
   HIPCK(hipMalloc(&g.d_dbg, kMaxZones * 8 * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * 8 * sizeof(unsigned long long), g.stream));
+  HIPCK(hipMalloc(&g.d_spawn_n, sizeof(unsigned int)));
+  HIPCK(hipMemsetAsync(g.d_spawn_n, 0, sizeof(unsigned int), g.stream));
+  HIPCK(hipMalloc(&g.d_tstart, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
+  HIPCK(hipMalloc(&g.d_tcnt, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
+  HIPCK(hipMalloc(&g.d_live, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
   if(R() > 1)
   {
@@ -667,6 +792,9 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   }
   g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
+  g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
+  g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;
+  for(int p = 0; p < 2; ++p) g.d_skey[p] = g.d_sarg[p] = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
@@ -735,7 +863,11 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
   HostType& t = g.types[type_id];
   if(!t.registered || t.created || count == 0) return GPU_ACTOR_EINVAL;
+  if(t.reserve && R() > 1) return GPU_ACTOR_EINVAL;
+  const uint64_t live = count;
+  count += t.reserve;                    // ids for the type's spawned actors
   if(g.n_actors + count > g.cfg.max_actors) return GPU_ACTOR_ERANGE;
+  if(g.spawn_cap + t.reserve > 0xFFFFFFFFull) return GPU_ACTOR_ERANGE;
   if(t.ht == GPU_ACTOR_HT_GUPS_UPDATER)
   {
     const uint64_t size = t.params[0];
@@ -759,14 +891,56 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   if(rc) return rc;
   rc = upload_types();
   if(rc) return rc;
-  if(t.lcount)
+  hipLaunchKernelGGL(k_construct, dim3(blocks_for(live)), dim3(kBlock), 0, g.stream,
+    type_id, (uint32_t)std::min<uint64_t>(live, t.lcount));
+  HIPCK(hipGetLastError());
+  const unsigned long long live_ull = live;
+  HIPCK(hipMemcpyAsync(g.d_live + type_id, &live_ull, sizeof(live_ull), hipMemcpyHostToDevice,
+    g.stream));
+  if(t.reserve)
   {
-    hipLaunchKernelGGL(k_construct, dim3(blocks_for(t.lcount)), dim3(kBlock), 0, g.stream,
-      type_id);
-    HIPCK(hipGetLastError());
+    // the spawn buffers hold one record per reserved id; nothing is in them
+    // between steps, so growing them drops nothing
+    HIPCK(hipStreamSynchronize(g.stream));
+    const uint32_t cap = g.spawn_cap + (uint32_t)t.reserve;
+    for(int p = 0; p < 2; ++p)
+    {
+      if(g.d_skey[p]) HIPCK(hipFree(g.d_skey[p]));
+      if(g.d_sarg[p]) HIPCK(hipFree(g.d_sarg[p]));
+      HIPCK(hipMalloc(&g.d_skey[p], (size_t)cap * sizeof(uint64_t)));
+      HIPCK(hipMalloc(&g.d_sarg[p], (size_t)cap * sizeof(uint64_t)));
+    }
+    g.spawn_cap = cap;
+    rc = upload_types();
+    if(rc) return rc;
   }
   HIPCK(hipStreamSynchronize(g.stream));
   if(first_id) *first_id = t.first;
+  return 0;
+}
+
+GPU_ACTOR_API int gpu_actor_type_reserve(uint32_t type_id, uint64_t n)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init) return GPU_ACTOR_ESTATE;
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !g.types[type_id].registered ||
+    g.types[type_id].created) return GPU_ACTOR_EINVAL;
+  if(n && R() > 1) return GPU_ACTOR_EINVAL;
+  if(n > g.cfg.max_actors) return GPU_ACTOR_ERANGE;
+  g.types[type_id].reserve = n;
+  return 0;
+}
+
+GPU_ACTOR_API int gpu_actor_type_live(uint32_t type_id, uint64_t* live)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init) return GPU_ACTOR_ESTATE;
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !live || !g.types[type_id].created)
+    return GPU_ACTOR_EINVAL;
+  unsigned long long v = 0;
+  HIPCK(hipMemcpyAsync(&v, g.d_live + type_id, sizeof(v), hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  *live = v;
   return 0;
 }
 

@@ -93,6 +93,12 @@ struct EngDev {
   unsigned long long* xcount;     // [nranks]
   uint32_t xcap, pad1;
   unsigned long long* dbg;        // [n_zones][8] phase stamps (diagnostic build)
+  // actors created by behaviours this step (gpu_actor_type_reserve): sort key
+  // type << 52 | creator << 20 | seq << 4 | beh, and the constructor's arg
+  uint64_t* spawn_key;
+  uint64_t* spawn_arg;
+  unsigned int* spawn_n;          // records written (may exceed spawn_cap: overflow)
+  uint32_t spawn_cap, pad3;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -152,6 +158,7 @@ struct ActorCtx {
   uint32_t sent;
   uint32_t applied;      // local reducible applies issued
   int      applied_type;
+  int      type;         // the draining actor's type
   ORec*     out;         // zone outbox (global scratch)
   uint32_t  ocap;        // its capacity
   uint32_t  nxt;         // landing parity of this step's sends
@@ -259,6 +266,30 @@ __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t b
   a.seq++;
 }
 
+// pony_create inside a behaviour + its constructor message (actor.c:688-734,
+// gencall.c:606-612): recorded with its canonical key; the id is assigned
+// when the step ends (engine.hip: spawn_process), the constructor message is
+// delivered in the next step. Counts as a send of the creator.
+__device__ __forceinline__ void spawn_actor(ActorCtx& a, uint32_t type, uint32_t beh, uint64_t arg)
+{
+  a.sent++;
+  if(a.seq >= kSeqMax)
+  {
+    atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
+    return;
+  }
+  const unsigned int pos = atomicAdd(c_eng.spawn_n, 1u);
+  if(pos < c_eng.spawn_cap)
+  {
+    c_eng.spawn_key[pos] = ((uint64_t)type << 52) | ((uint64_t)a.self << 20) |
+                           ((uint64_t)a.seq << 4) | (beh & 0xFu);
+    c_eng.spawn_arg[pos] = arg;
+  }
+  else
+    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+  a.seq++;
+}
+
 __device__ __forceinline__ bool is_remote(uint32_t to)
 {
   return c_eng.nranks > 1 && rmod(to) != c_eng.rank;
@@ -357,6 +388,7 @@ template <> struct HT_Words<GPU_ACTOR_HT_GUPS_STREAMER> { static constexpr int W
 template <> struct HT_Words<GPU_ACTOR_HT_STORM>         { static constexpr int W = 2; };
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SRC>      { static constexpr int W = 3; };
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SINK>     { static constexpr int W = 11; };
+template <> struct HT_Words<GPU_ACTOR_HT_SPREADER>      { static constexpr int W = 5; };
 
 template <int HT>
 __device__ __forceinline__ void handle(const TypeDev& T, ActorCtx& a, uint64_t (&s)[HT_Words<HT>::W],
@@ -498,6 +530,41 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_FIFO_SINK>(const TypeDev& T,
   if(seq != last + 1) s[2] += 1;
 #pragma unroll
   for(int k = 0; k < 8; ++k) s[3 + k] = (slot == (uint32_t)k) ? seq : s[3 + k];
+}
+
+// examples/spreader/main.pony:9-48
+template <>
+__device__ __forceinline__ void handle<GPU_ACTOR_HT_SPREADER>(const TypeDev& T, ActorCtx& a,
+  uint64_t (&s)[5], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+{
+  if(beh == GPU_ACTOR_SPREADER_SPREAD)
+  {
+    // new create(env) / new spread(parent, count)
+    const uint64_t parent = arg >> 32, count = arg & 0xFFFFFFFFull;
+    s[0] = count;
+    s[1] = parent == 0xFFFFFFFFull ? GPU_ACTOR_NONE : parent;
+    if(count <= 1)
+    {
+      if(s[1] != GPU_ACTOR_NONE) send_serial(a, (uint32_t)s[1], GPU_ACTOR_SPREADER_RESULT, 1);
+      else s[4] = 1;                                     // "1 actor"
+    }
+    else
+    {
+      // spawn_child() twice: Spreader.spread(this, _count - 1)
+      const uint64_t ctor = ((uint64_t)a.self << 32) | (count - 1);
+      spawn_actor(a, (uint32_t)a.type, GPU_ACTOR_SPREADER_SPREAD, ctor);
+      spawn_actor(a, (uint32_t)a.type, GPU_ACTOR_SPREADER_SPREAD, ctor);
+    }
+    return;
+  }
+  // be result(i)
+  s[3] += 1;
+  s[2] += arg;
+  if(s[3] == 2)
+  {
+    if(s[1] != GPU_ACTOR_NONE) send_serial(a, (uint32_t)s[1], GPU_ACTOR_SPREADER_RESULT, s[2] + 1);
+    else s[4] = s[2] + 1;                               // "<n> actors"
+  }
 }
 
 } // namespace gpa

@@ -538,6 +538,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     a.li = L - T.lfirst;
     a.self = L * R + me;
     a.src_local = i;
+    a.type = t;
     a.seq = 0;
     const uint32_t co = s_aux[i];
     const uint32_t room = co < cap ? cap - co : 0u;
@@ -567,6 +568,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         ZCASE(GPU_ACTOR_HT_STORM)
         ZCASE(GPU_ACTOR_HT_FIFO_SRC)
         ZCASE(GPU_ACTOR_HT_FIFO_SINK)
+        ZCASE(GPU_ACTOR_HT_SPREADER)
 #undef ZCASE
         default: break;
       }

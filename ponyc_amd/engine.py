@@ -29,6 +29,8 @@ FANIN_SEND_MSGS, FANIN_MSG = 0, 0
 GUPS_APPLY, GUPS_UPDATE = 0, 0
 STORM_TOKEN, STORM_STORM = 0, 1
 FIFO_BURST, FIFO_PUSH = 0, 0
+HT_SPREADER = 11
+SPREADER_SPREAD, SPREADER_RESULT = 0, 1
 NONE_ID = 0xFFFFFFFFFFFFFFFF
 
 ERRORS = {
@@ -73,7 +75,8 @@ class Counts(ctypes.Structure):
 EXPORTS = [
     "gpu_actor_init", "gpu_actor_shutdown", "gpu_actor_comm_id",
     "gpu_actor_type_register", "gpu_actor_type_config", "gpu_actor_type_param",
-    "gpu_actor_create", "gpu_actor_alloc_msgs", "gpu_actor_sendv", "gpu_actor_send",
+    "gpu_actor_create", "gpu_actor_type_reserve", "gpu_actor_type_live",
+    "gpu_actor_alloc_msgs", "gpu_actor_sendv", "gpu_actor_send",
     "gpu_actor_run", "gpu_actor_run_fixed", "gpu_actor_sync",
     "gpu_actor_state_read", "gpu_actor_state_write", "gpu_actor_counts",
     "gpu_actor_owner", "gpu_actor_stream", "gpu_actor_last_drain_ms", "gpu_actor_strerror",
@@ -109,6 +112,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "gpu_actor_type_config": (i32, [u32, u32, u32]),
         "gpu_actor_type_param": (i32, [u32, u32, u64]),
         "gpu_actor_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
+        "gpu_actor_type_reserve": (i32, [u32, u64]),
+        "gpu_actor_type_live": (i32, [u32, ctypes.POINTER(u64)]),
         "gpu_actor_alloc_msgs": (i32, [u64, ctypes.POINTER(vp)]),
         "gpu_actor_sendv": (i32, [vp, u64]),
         "gpu_actor_send": (i32, [u64, u32, u64]),
@@ -209,6 +214,7 @@ class Engine:
         self.words: dict[int, int] = {}
         self.first: dict[int, int] = {}
         self.count: dict[int, int] = {}
+        self.reserve: dict[int, int] = {}
         self.alive = True
 
     @staticmethod
@@ -231,11 +237,21 @@ class Engine:
         _ck("gpu_actor_type_param",
             self.lib.gpu_actor_type_param(type_id, idx, int(value) & 0xFFFFFFFFFFFFFFFF))
 
+    def type_reserve(self, type_id: int, n: int) -> None:
+        """Room for n actors that behaviours spawn while running."""
+        _ck("gpu_actor_type_reserve", self.lib.gpu_actor_type_reserve(type_id, n))
+        self.reserve[type_id] = n
+
+    def type_live(self, type_id: int) -> int:
+        v = ctypes.c_uint64(0)
+        _ck("gpu_actor_type_live", self.lib.gpu_actor_type_live(type_id, ctypes.byref(v)))
+        return v.value
+
     def create(self, type_id: int, count: int) -> int:
         first = ctypes.c_uint64(0)
         _ck("gpu_actor_create", self.lib.gpu_actor_create(type_id, count, ctypes.byref(first)))
         self.first[type_id] = first.value
-        self.count[type_id] = count
+        self.count[type_id] = count + self.reserve.get(type_id, 0)   # id range incl. reserve
         return first.value
 
     # -- sending -------------------------------------------------------------

@@ -14,7 +14,8 @@ import numpy as np
 from .engine import (MSG_DTYPE, HT_RING, HT_PINGER, HT_PINGER_DET, HT_FANIN_SENDER,
                      HT_FANIN_ANALYZER, HT_GUPS_STREAMER, HT_GUPS_UPDATER, HT_STORM,
                      HT_FIFO_SRC, HT_FIFO_SINK, RING_SET, RING_PASS, PINGER_PING,
-                     FANIN_SEND_MSGS, GUPS_APPLY, STORM_TOKEN, STORM_STORM, FIFO_BURST)
+                     FANIN_SEND_MSGS, GUPS_APPLY, STORM_TOKEN, STORM_STORM, FIFO_BURST,
+                     HT_SPREADER, SPREADER_SPREAD)
 
 
 def _msgs(to, beh, arg) -> np.ndarray:
@@ -152,6 +153,24 @@ def storm(eng, n: int, r: int = 4, hops: int = 16, seed: int = 5489, type_id: in
                            (i * np.uint64(r) + np.uint64(k)) << np.uint64(32)))
     eng.sendv(np.concatenate(parts))
     return {"type": type_id, "first": first, "n": n}
+
+
+# ---- examples/spreader ---------------------------------------------------------------------
+def spreader(eng, count: int = 10, type_id: int = 0) -> dict:
+    """Main + Spreader(env) (spreader/main.pony:50-52, 9-19): one root actor;
+    every node spawns two children until count reaches 1, so the tree has
+    2^count - 1 actors, all but the root spawned by behaviours."""
+    eng.type_register(type_id, 5, HT_SPREADER)
+    nodes = (1 << count) - 1
+    eng.type_reserve(type_id, nodes - 1)
+    root = eng.create(type_id, 1)
+    eng.send(root, SPREADER_SPREAD, (0xFFFFFFFF << 32) | count)
+    return {"type": type_id, "root": root, "nodes": nodes}
+
+
+def spreader_result(eng, w: dict) -> np.ndarray:
+    """[count, parent, _result, _received, printed] of every actor, by id."""
+    return eng.state_read(w["type"])
 
 
 # ---- per-pair FIFO probe ---------------------------------------------------------------------

@@ -10,7 +10,7 @@
   * manifest.json   : configs, seeds and totals.
 
 Run from the repo root in the build container (needs /root/reference):
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py [fixture names...]   (default: all)
 """
 from __future__ import annotations
 
@@ -46,6 +46,8 @@ CONFIGS = [
                                           "chunk": 1024, "iterate": 10}, ["table"]),
     ("fifo_64_8_b10_m4", "fifo", {"sources": 64, "sinks": 8, "bursts": 10, "m": 4},
      ["h", "n", "violations"]),
+    # every node's final _result (sorted: ids are runtime pointers) + the root's total
+    ("spreader_c12", "spreader", {"count": 12}, ["results_sorted", "total"]),
 ]
 
 
@@ -61,15 +63,23 @@ def extract_kats() -> dict:
 
 def main() -> None:
     pyoracle.build(reference=True)
+    only = set(sys.argv[1:])
     manifest = {"generator": "tests/golden/gen_golden.py",
                 "reference": "KittyMac/ponyc src/libponyrt @ VERSION 0.33.0, unmodified",
                 "threads": 4, "fixtures": {}}
-    kats = extract_kats()
-    with open(os.path.join(HERE, "rng_kats.json"), "w") as f:
-        json.dump(kats, f, indent=1)
+    mpath = os.path.join(HERE, "manifest.json")
+    if only and os.path.exists(mpath):
+        with open(mpath) as f:
+            manifest = json.load(f)
+    if not only:
+        kats = extract_kats()
+        with open(os.path.join(HERE, "rng_kats.json"), "w") as f:
+            json.dump(kats, f, indent=1)
     tmp = os.path.join(HERE, "_tmp")
     os.makedirs(tmp, exist_ok=True)
     for name, harness, args, fields in CONFIGS:
+        if only and name not in only:
+            continue
         a = dict(args)
         a["threads"] = 4
         out = os.path.join(tmp, name + ".bin")

@@ -137,3 +137,55 @@ def test_mailbox_overflow_reported(engine_factory):
     with pytest.raises(GpuActorError) as ei:
         e2.run()
     assert ei.value.code == -4
+
+
+# ---- actors created by behaviours (examples/spreader) -------------------
+@pytest.mark.parametrize("count", [1, 2, 5, 12, 16])
+def test_spreader(engine_factory, oracle, count):
+    """Every actor but the root is spawned on the device; ids follow the
+    canonical (creator, seq) order, so the whole state matches the oracle."""
+    g, o = _both(engine_factory, oracle, lambda e: W.spreader(e, count), W.spreader_result)
+    _assert_same(g, o)
+    st = g[2]
+    nodes = (1 << count) - 1
+    assert int(st[4][0]) == nodes                       # the root prints 2^count - 1 actors
+
+
+def test_spreader_matches_reference_golden(engine_factory):
+    """Against the reference runtime's own run (tests/golden/spreader_c12)."""
+    from test_oracle_golden import spreader_view, expected
+    e = engine_factory()
+    w = W.spreader(e, 12)
+    e.run()
+    np.testing.assert_array_equal(spreader_view(W.spreader_result(e, w), w),
+                                  expected("spreader_c12"))
+    assert e.type_live(w["type"]) == w["nodes"]
+
+
+def test_spreader_after_other_types(engine_factory, oracle):
+    """Spawned ids sit inside their own type's range with other types around
+    it; the ring's traffic runs in the same steps."""
+    def setup(e):
+        r = W.ring(e, 100, 3, 50, type_id=0)
+        s = W.spreader(e, 9, type_id=1)
+        W.fanin(e, 200, 2, 5, an_type=2, snd_type=3)
+        return r, s
+    def result(e, w):
+        r, s = w
+        return np.concatenate([W.ring_result(e, r).ravel(), W.spreader_result(e, s).ravel(),
+                               e.state_read(2).ravel()])
+    g, o = _both(engine_factory, oracle, setup, result)
+    _assert_same(g, o)
+
+
+def test_spreader_reserve_exhausted(engine_factory):
+    """Spawning past the reserve is reported like a dropped message."""
+    from ponyc_amd.engine import GpuActorError
+    e = engine_factory()
+    e.type_register(0, 5, W.HT_SPREADER)
+    e.type_reserve(0, 10)
+    root = e.create(0, 1)
+    e.send(root, W.SPREADER_SPREAD, (0xFFFFFFFF << 32) | 6)
+    with pytest.raises(GpuActorError):
+        e.run()
+    assert e.type_live(0) == 11

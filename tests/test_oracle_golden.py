@@ -42,7 +42,17 @@ def setup_from(name, eng):
     if h == "fifo":
         w = W.fifo(eng, a["sources"], a["sinks"], a["bursts"], a["m"])
         return w, lambda: W.fifo_result(eng, w)
+    if h == "spreader":
+        w = W.spreader(eng, a["count"])
+        return w, lambda: spreader_view(W.spreader_result(eng, w), w)
     raise KeyError(h)
+
+
+def spreader_view(st, w):
+    """The harness's layout: node results sorted, then the root's total."""
+    tot = np.zeros(w["nodes"], dtype=np.uint64)
+    tot[0] = st[4][0]                     # the root is the type's first actor
+    return np.stack([np.sort(st[2][:w["nodes"]]), tot])
 
 
 def expected(name):
