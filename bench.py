@@ -37,6 +37,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PINGER_STATE_BYTES = 24        # rng x, y + count
+# PMC summary (scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of the current k_step build
+PMC_TAG = "r01c"
 REC_BYTES = 16
 
 
@@ -198,7 +200,7 @@ def main():
     alg_bytes = msgs_per_step * 2 * REC_BYTES + active_per_step * 2 * PINGER_STATE_BYTES
     achieved = alg_bytes / (drain_ms * 1e-3) / 1e9 if drain_ms > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_step_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_step_%s.json" % PMC_TAG)
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
