@@ -14,9 +14,11 @@ the K timed steps.
 Also reported:
   roofline     — the drain kernel's algorithmic HBM bytes per launch
                  (32 B per message: 16-B record written by the sender's zone and
-                 read by the receiver's zone; 2*S per active actor: state read +
-                 write, S = 24 B for a pinger) / its HIP-event-timed average
-                 duration (k_step, on the engine's stream);
+                 read by the receiver's zone; 2*S + 2*M per active actor: state
+                 read + write, S = 24 B for a pinger, and the mailbox head/tail
+                 M = 8 B — SURVEY §8 d3's formula) / its average duration,
+                 timed by HIP events bound to every 8th k_step dispatch of the
+                 timed region (hipExtLaunchKernel, on the engine's stream);
   cpu_baseline — the reference runtime (oracle/_ref/libponyrt.so, built from
                  KittyMac/ponyc src/libponyrt) running the same pinger graph via
                  oracle/_ref/harness_ubench on this host's cores (rank 0, N=1).
@@ -40,6 +42,7 @@ PINGER_STATE_BYTES = 24        # rng x, y + count
 # PMC summary (scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of the current k_step build
 PMC_TAG = "r01c"
 REC_BYTES = 16
+MAILBOX_BYTES = 8              # mailbox head/tail per active actor (SURVEY §8 d3's M)
 
 
 def parse():
@@ -197,7 +200,9 @@ def main():
     # roofline of the drain kernel on this rank (per launch)
     msgs_per_step = delivered / args.steps / world
     active_per_step = active / args.steps / world
-    alg_bytes = msgs_per_step * 2 * REC_BYTES + active_per_step * 2 * PINGER_STATE_BYTES
+    # B = sum_msgs 2R + sum_active_actors (2S + 2M)
+    alg_bytes = (msgs_per_step * 2 * REC_BYTES
+                 + active_per_step * (2 * PINGER_STATE_BYTES + 2 * MAILBOX_BYTES))
     achieved = alg_bytes / (drain_ms * 1e-3) / 1e9 if drain_ms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step_%s.json" % PMC_TAG)

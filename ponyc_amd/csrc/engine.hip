@@ -8,6 +8,7 @@
 // The launch boundary is the BSP barrier; quiescence ("no pending mail on any
 // rank") replaces the CNF/ACK protocol (scheduler.c:303-480).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
@@ -553,11 +554,17 @@ int spawn_process(uint32_t cur)
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
-  if(e0) HIPCK(hipEventRecord(e0, g.stream));
   const size_t dyn = 4 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
   step_kernel_t kern = pick_step_kernel();
-  hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
-  if(e1) HIPCK(hipEventRecord(e1, g.stream));
+  if(e0)
+  {
+    // the events take the dispatch's own start/end timestamps: no marker
+    // packets between steps
+    hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), (uint32_t)dyn, g.stream,
+      e0, e1, 0u, g.par, slot);
+  }
+  else
+    hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
   HIPCK(hipGetLastError());
   g.par ^= 1u;
   if(R() > 1)
@@ -597,6 +604,8 @@ int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out)
     return GPU_ACTOR_ECOMM;
   return 0;
 }
+
+constexpr uint64_t kEventStride = 8;
 
 int ensure_events(size_t n)
 {
@@ -1024,14 +1033,19 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(g.n_zones == 0 || n == 0) return 0;
-  const uint64_t timed = std::min<uint64_t>(n, 2048);
-  int rc = ensure_events(2 * timed);
+  // Every kEventStride-th step carries start/stop events (the dispatch's own
+  // timestamps, hipExtLaunchKernel); timing every step costs ~5 us of
+  // inter-kernel gap per step (measured: 92.3 vs 87.4 us per C2 step).
+  static const int stride_env = getenv("GPA_EVENT_STRIDE") ? atoi(getenv("GPA_EVENT_STRIDE")) : 0;
+  const uint64_t stride = stride_env > 0 ? (uint64_t)stride_env : kEventStride;
+  const uint64_t timed = std::min<uint64_t>((n + stride - 1) / stride, 2048);
+  int rc = ensure_events(2 * std::max<uint64_t>(timed, 1));
   if(rc) return rc;
   HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
   for(uint64_t j = 0; j < n; ++j)
   {
-    const bool tm = j >= n - timed;
-    const uint64_t e = j - (n - timed);
+    const uint64_t e = j / stride;
+    const bool tm = (j % stride) == 0 && e < timed;
     rc = launch_step((uint32_t)(j % kPendPre), tm ? g.ev[2 * e] : nullptr,
       tm ? g.ev[2 * e + 1] : nullptr);
     if(rc) return rc;
