@@ -43,6 +43,9 @@ PINGER_STATE_BYTES = 24        # rng x, y + count
 PMC_TAG = "r01c"
 REC_BYTES = 16
 MAILBOX_BYTES = 8              # mailbox head/tail per active actor (SURVEY §8 d3's M)
+# device atomic peak measured on MI355X by scripts/ubench_mem.hip (random u32
+# atomicAdd over 1M counters; profiles/r01e_ubench_mem.txt)
+ATOMIC_PEAK_GOPS = 26.3
 
 
 def parse():
@@ -194,6 +197,7 @@ def main():
     secs = allmax(pg, local_secs)
     delivered = c1["delivered"] - c0["delivered"]
     active = c1["active"] - c0["active"]
+    atomics = c1["atomics"] - c0["atomics"]
     dropped = c1["dropped"]
     eng.shutdown()
 
@@ -240,6 +244,15 @@ def main():
                 "exchange": exchange,
             },
             "msgs_per_step": round(delivered / args.steps, 1),
+            # global atomics (chunk reservations, one per
+            # (zone, destination bucket) per step; counted on device) per
+            # delivered message, and their rate against the measured device peak
+            "atomics": {
+                "per_msg": round(atomics / max(delivered, 1), 5),
+                "gops": round(atomics / world / args.steps / (drain_ms * 1e-3) / 1e9, 3)
+                if drain_ms > 0 else None,
+                "peak_gops": ATOMIC_PEAK_GOPS,
+            },
             "dropped": dropped,
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

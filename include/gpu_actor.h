@@ -48,6 +48,7 @@ extern "C" {
 #define GPU_ACTOR_ESTATE       -6   /* not initialised / already initialised   */
 #define GPU_ACTOR_ERANGE       -7   /* sequence or id space exhausted          */
 #define GPU_ACTOR_ECOMM        -8   /* RCCL / exchange failure                 */
+#define GPU_ACTOR_EBUSY        -9   /* an asynchronous run is in flight         */
 
 #define GPU_ACTOR_MAX_TYPES    16
 #define GPU_ACTOR_MAX_PARAMS   8
@@ -86,6 +87,8 @@ typedef struct gpu_actor_counts_t
   uint64_t remote;      /* messages that crossed ranks                       */
   uint64_t active;      /* actor-steps that handled at least one message     */
   uint64_t delivered_by_type[GPU_ACTOR_MAX_TYPES];
+  uint64_t atomics;     /* global chunk-reservation atomics the drain kernel
+                           issued (one per (zone, destination bucket) per step) */
 } gpu_actor_counts_t;
 
 /* ---- lifecycle (pony_init / pony_start / pony_stop, pony.h:486-559) ------ */
@@ -154,6 +157,21 @@ GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done);
 GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n);
 /* Block until all queued device work is done; returns the sticky error. */
 GPU_ACTOR_API int gpu_actor_sync(void);
+/* Asynchronous run (the ASIO delivery pattern, event.c:116-135):
+ * gpu_actor_run(max_steps) on a library progress thread; returns at once.
+ * When the run ends, done(ctx, rc, steps_done) is called ON THAT THREAD,
+ * outside the library's lock (it may call back into the library). A Pony
+ * binding's `done` calls pony_register_thread() (pony.h:520-528) once and then
+ * pony_sendv_single()s a completion message to the notify actor passed as ctx
+ * (INTEGRATION.md). While the run is in flight the other entry points block
+ * behind it (calls are serialised), and gpu_actor_run/run_async return
+ * GPU_ACTOR_EBUSY. done may be NULL (poll gpu_actor_busy / gpu_actor_wait). */
+typedef void (*gpu_actor_done_fn)(void* ctx, int rc, uint64_t steps_done);
+GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done, void* ctx);
+/* Join the last asynchronous run: its return code and steps (0 if none). */
+GPU_ACTOR_API int gpu_actor_wait(uint64_t* steps_done);
+/* 1 while an asynchronous run is in flight, else 0. */
+GPU_ACTOR_API int gpu_actor_busy(void);
 
 /* ---- state and counters ------------------------------------------------- */
 /* Copy state of actors [first, first+n) of a type (indices relative to the

@@ -16,7 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "engine_dev.h"
@@ -164,6 +166,11 @@ struct HostType {
 
 struct Engine {
   std::mutex mu;
+  // asynchronous run (gpu_actor_run_async): one progress thread at a time
+  std::thread worker;
+  bool async_busy = false;
+  int async_rc = 0;
+  uint64_t async_steps = 0;
   bool init = false;
   gpu_actor_config_t cfg{};
   int device = 0;
@@ -705,6 +712,7 @@ GPU_ACTOR_API const char* gpu_actor_strerror(int code)
     case GPU_ACTOR_ESTATE: return "engine not initialised or already initialised";
     case GPU_ACTOR_ERANGE: return "sequence or id space exhausted";
     case GPU_ACTOR_ECOMM: return "RCCL exchange failure";
+    case GPU_ACTOR_EBUSY: return "an asynchronous run is in flight";
     default: return "unknown error";
   }
 }
@@ -785,8 +793,15 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   return 0;
 }
 
+// Joins a finished (or running) asynchronous run; caller must NOT hold g.mu.
+void join_worker()
+{
+  if(g.worker.joinable()) g.worker.join();
+}
+
 GPU_ACTOR_API int gpu_actor_shutdown(void)
 {
+  join_worker();                      // an async run finishes first
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(g.stream) (void)hipStreamSynchronize(g.stream);
@@ -986,9 +1001,9 @@ GPU_ACTOR_API int gpu_actor_send(uint64_t to, uint32_t behaviour, uint64_t arg)
   return sendv_locked(&m, 1);
 }
 
-GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
+// The scheduler loop to quiescence (or max_steps); caller holds g.mu.
+int run_locked(uint64_t max_steps, uint64_t* steps_done)
 {
-  std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
   uint64_t done = 0;
   if(g.n_zones)
@@ -1026,6 +1041,67 @@ GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
   if(steps_done) *steps_done = done;
   g.host_seq = 0;     // a new host window starts after each run
   return check_sticky();
+}
+
+GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(g.async_busy) return GPU_ACTOR_EBUSY;
+  return run_locked(max_steps, steps_done);
+}
+
+GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done, void* ctx)
+{
+  {
+    std::lock_guard<std::mutex> lk(g.mu);
+    if(!g.init) return GPU_ACTOR_ESTATE;
+    if(g.async_busy) return GPU_ACTOR_EBUSY;
+  }
+  join_worker();                      // reap the previous, finished run
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(g.async_busy) return GPU_ACTOR_EBUSY;
+  g.async_busy = true;
+  g.async_rc = 0;
+  g.async_steps = 0;
+  const int dev = g.device;
+  try
+  {
+    g.worker = std::thread([max_steps, done, ctx, dev]() {
+      int rc;
+      uint64_t steps = 0;
+      {
+        std::lock_guard<std::mutex> wl(g.mu);
+        rc = hipSetDevice(dev) == hipSuccess ? run_locked(max_steps, &steps) : GPU_ACTOR_EHIP;
+        g.async_rc = rc;
+        g.async_steps = steps;
+        g.async_busy = false;
+      }
+      // outside the lock: the callback may call back into the library
+      if(done) done(ctx, rc, steps);
+    });
+  }
+  catch(...)
+  {
+    g.async_busy = false;
+    return GPU_ACTOR_ENOMEM;
+  }
+  return 0;
+}
+
+GPU_ACTOR_API int gpu_actor_wait(uint64_t* steps_done)
+{
+  join_worker();
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(steps_done) *steps_done = g.async_steps;
+  const int rc = g.async_rc;
+  g.async_rc = 0;
+  return rc;
+}
+
+GPU_ACTOR_API int gpu_actor_busy(void)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  return g.async_busy ? 1 : 0;
 }
 
 GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
@@ -1134,6 +1210,7 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
     out->remote = g.remote_total;
     out->active = st[ST_ACTIVE];
     for(int t = 0; t < GPU_ACTOR_MAX_TYPES; ++t) out->delivered_by_type[t] = st[ST_BY_TYPE + t];
+    out->atomics = st[ST_ATOMICS];
     return 0;
   }
   if(R() > 1)
@@ -1158,6 +1235,7 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   out->remote = g.remote_total;
   out->active = st[ST_ACTIVE];
   for(int t = 0; t < GPU_ACTOR_MAX_TYPES; ++t) out->delivered_by_type[t] = st[ST_BY_TYPE + t];
+  out->atomics = st[ST_ATOMICS];
   return 0;
 }
 

@@ -23,10 +23,18 @@ namespace gpa {
 
 constexpr int      kBlock = 256;                 // helper kernels
 constexpr int      kWaves = kBlock / 64;
-constexpr int      kZoneBits = 11;               // to_local field holds up to 12 bits
+// Zone geometry (A/B builds override it: scripts/build_variants.sh)
+#ifndef GPA_ZONE_BITS
+#define GPA_ZONE_BITS 11
+#endif
+#ifndef GPA_ZONE_THREADS
+#define GPA_ZONE_THREADS 512
+#endif
+constexpr int      kZoneBits = GPA_ZONE_BITS;    // to_local field holds up to 12 bits
+static_assert(kZoneBits <= 12, "to_local is 12 bits of a ZRec's w0");
 constexpr uint32_t kZone = 1u << kZoneBits;      // actors per zone
 constexpr uint32_t kZoneMask = kZone - 1;
-constexpr int      kZoneThreads = 512;           // one workgroup per zone
+constexpr int      kZoneThreads = GPA_ZONE_THREADS;  // one workgroup per zone
 constexpr int      kZoneWaves = kZoneThreads / 64;
 constexpr uint32_t kMaxZones = 4096;             // histogram bound (8M actors/rank)
 constexpr uint32_t kMaxRanks = 64;
@@ -38,6 +46,7 @@ constexpr uint32_t kFanLds = 256;                // analyzers a zone accumulates
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
   ST_SEQ_OVERFLOW = 5, ST_XCHG_OVERFLOW = 6, ST_ACTIVE = 7,
+  ST_ATOMICS = 8,        // global reservation atomics issued by k_step
   ST_BY_TYPE = 16, ST_COUNT = 32
 };
 

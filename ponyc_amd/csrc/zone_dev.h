@@ -38,10 +38,17 @@ namespace gpa {
 #endif
 
 constexpr int kUnroll = 8;   // independent records in flight per thread in streaming loops
-constexpr uint32_t kIdxCap = 16384;   // LDS index budget per zone (records per step)
-constexpr uint32_t kTile = 4096;      // outbox records sorted per scatter tile (64 KB of LDS)
-constexpr int kTilePer = kTile / 512; // tile records per thread
-constexpr int kIdxPer = kIdxCap / 512; // landed records per thread on the LDS-index path
+#ifndef GPA_IDX_CAP
+#define GPA_IDX_CAP 16384
+#endif
+#ifndef GPA_TILE
+#define GPA_TILE 4096
+#endif
+constexpr uint32_t kIdxCap = GPA_IDX_CAP;  // LDS index budget per zone (records per step)
+constexpr uint32_t kTile = GPA_TILE;       // outbox records sorted per scatter tile (64 KB of LDS)
+constexpr int kTilePer = kTile / kZoneThreads;  // tile records per thread
+constexpr int kIdxPer = kIdxCap / kZoneThreads; // landed records per thread on the LDS-index path
+static_assert(kTile % kZoneThreads == 0 && kIdxCap % kZoneThreads == 0, "tile / index split");
 // Arrival groups up to this size are loaded at once and ordered in registers.
 // 16 where the handler does not read the message (pinger: the selection
 // compiles away) or the table's state is small; 8 elsewhere, to stay within
@@ -622,11 +629,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // ---- 4. one chunk per destination bucket ----------------------------------------
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
+  uint32_t n_atom = 0;
   for(uint32_t b = tid; b < nb; b += kZoneThreads)
   {
     const uint32_t h = s_hist[b];
     if(h)
     {
+      ++n_atom;
       if(b < nz)
         s_base[b] = atomicAdd(&c_eng.land_n[nxt][b], h);
       else
@@ -716,21 +725,21 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
 
   // ---- counters: block reduction, one atomic per workgroup per counter ---------------
-  unsigned long long v[6] = { delivered + applied, sent, active, dropped, xover, 0 };
+  unsigned long long v[6] = { delivered + applied, sent, active, dropped, xover, n_atom };
 #pragma unroll
-  for(int k = 0; k < 5; ++k)
+  for(int k = 0; k < 6; ++k)
   {
     v[k] = wave_sum(v[k]);
     if(lane == 0) s_red[wv][k] = v[k];
   }
   __syncthreads();
   GPA_STAMP(6);
-  if(tid < 5)
+  if(tid < 6)
   {
     unsigned long long tot = 0;
     for(int w = 0; w < kZoneWaves; ++w) tot += s_red[w][tid];
     const int idx = tid == 0 ? ST_DELIVERED : tid == 1 ? ST_SENT : tid == 2 ? ST_ACTIVE
-                  : tid == 3 ? ST_DROPPED : ST_XCHG_OVERFLOW;
+                  : tid == 3 ? ST_DROPPED : tid == 4 ? ST_XCHG_OVERFLOW : ST_ATOMICS;
     if(tot) atomicAdd(&c_eng.stats[idx], tot);
   }
 }

@@ -68,6 +68,7 @@ class Counts(ctypes.Structure):
         ("remote", ctypes.c_uint64),
         ("active", ctypes.c_uint64),
         ("delivered_by_type", ctypes.c_uint64 * MAX_TYPES),
+        ("atomics", ctypes.c_uint64),
     ]
 
 
@@ -80,7 +81,7 @@ EXPORTS = [
     "gpu_actor_run", "gpu_actor_run_fixed", "gpu_actor_sync",
     "gpu_actor_state_read", "gpu_actor_state_write", "gpu_actor_counts",
     "gpu_actor_owner", "gpu_actor_stream", "gpu_actor_last_drain_ms", "gpu_actor_strerror",
-    "gpu_actor_set_transport",
+    "gpu_actor_set_transport", "gpu_actor_run_async", "gpu_actor_wait", "gpu_actor_busy",
 ]
 
 # host-transport callbacks (include/gpu_actor.h: gpu_actor_alltoallv_fn / _allreduce_fn)
@@ -89,6 +90,8 @@ ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.POINTER(ctypes.c_uint64))
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64)
+# completion callback of gpu_actor_run_async (include/gpu_actor.h: gpu_actor_done_fn)
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
 
 _lib = None
 
@@ -128,6 +131,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "gpu_actor_last_drain_ms": (ctypes.c_double, []),
         "gpu_actor_strerror": (ctypes.c_char_p, [i32]),
         "gpu_actor_set_transport": (i32, [ALLTOALLV_FN, ALLREDUCE_FN, vp]),
+        "gpu_actor_run_async": (i32, [u64, DONE_FN, vp]),
+        "gpu_actor_wait": (i32, [ctypes.POINTER(u64)]),
+        "gpu_actor_busy": (i32, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -272,6 +278,25 @@ class Engine:
         _ck("gpu_actor_run", self.lib.gpu_actor_run(max_steps, ctypes.byref(steps)))
         return steps.value
 
+    def run_async(self, max_steps: int = 0, done=None) -> None:
+        """gpu_actor_run on the library's progress thread; done(rc, steps) is
+        called on that thread when the run ends (the Pony binding sends a
+        completion message to a notify actor from there)."""
+        def _cb(_ctx, rc, steps):
+            if done is not None:
+                done(rc, steps)
+        self._done_cb = DONE_FN(_cb)      # kept alive until the next run_async
+        _ck("gpu_actor_run_async", self.lib.gpu_actor_run_async(max_steps, self._done_cb, None))
+
+    def wait(self) -> int:
+        """Join the last asynchronous run; returns its step count."""
+        steps = ctypes.c_uint64(0)
+        _ck("gpu_actor_wait", self.lib.gpu_actor_wait(ctypes.byref(steps)))
+        return steps.value
+
+    def busy(self) -> bool:
+        return bool(self.lib.gpu_actor_busy())
+
     def run_fixed(self, n: int) -> None:
         _ck("gpu_actor_run_fixed", self.lib.gpu_actor_run_fixed(n))
 
@@ -314,6 +339,7 @@ class Engine:
             "pending": c.pending, "dropped": c.dropped, "remote": c.remote,
             "active": c.active,
             "delivered_by_type": [c.delivered_by_type[i] for i in range(MAX_TYPES)],
+            "atomics": c.atomics,
         }
 
     def stream(self) -> int:

@@ -7,6 +7,8 @@ b() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -
 for v in "$@"; do
   case $v in
     base) b base ;;
+    z12a) b z12a -DGPA_ZONE_BITS=12 -DGPA_ZONE_THREADS=1024 -DGPA_IDX_CAP=24576 -DGPA_TILE=7168 ;;
+    z12b) b z12b -DGPA_ZONE_BITS=12 -DGPA_ZONE_THREADS=1024 -DGPA_IDX_CAP=32768 -DGPA_TILE=8192 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

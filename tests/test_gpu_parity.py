@@ -189,3 +189,28 @@ def test_spreader_reserve_exhausted(engine_factory):
     with pytest.raises(GpuActorError):
         e.run()
     assert e.type_live(0) == 11
+
+
+def test_run_async_completion(engine_factory, oracle):
+    """gpu_actor_run_async: the run happens on the library's
+    progress thread and its completion callback reports the same step count
+    as the synchronous oracle run; state is bit-exact afterwards."""
+    import threading
+    e = engine_factory()
+    we = W.ubench(e, 4096, 4, det=True, hops=32)
+    fired = threading.Event()
+    got = {}
+
+    def done(rc, steps):
+        got["rc"], got["steps"] = rc, steps
+        fired.set()
+    e.run_async(0, done)
+    assert fired.wait(60), "completion callback never fired"
+    assert e.wait() == got["steps"]
+    assert got["rc"] == 0
+    assert not e.busy()
+    wo = W.ubench(oracle, 4096, 4, det=True, hops=32)
+    so = oracle.run()
+    assert got["steps"] == so
+    np.testing.assert_array_equal(W.ubench_result(e, we), W.ubench_result(oracle, wo))
+    assert e.counts()["delivered"] == oracle.counts()["delivered"]
