@@ -65,3 +65,32 @@ def test_engine_refuses_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(engine, "_lib", None)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         engine.load_library(str(tmp_path / "missing.so"))
+
+
+def _arity(sig: str) -> int:
+    depth, n, seen = 0, 0, False
+    for ch in sig:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        elif ch == "," and depth == 0:
+            n += 1
+        elif not ch.isspace():
+            seen = True
+    return n + 1 if seen and sig.strip() not in ("void",) else 0
+
+
+def test_pony_package_binds_the_header():
+    """pony/gpu_actor (not compilable here, ponyc needs LLVM <= 7)
+    declares every entry point a Pony program uses, each with the header's
+    arity, and nothing the library does not export."""
+    pony = open(os.path.join(ROOT, "pony", "gpu_actor", "gpu_actor.pony")).read()
+    decl = dict(re.findall(r"^use @(gpu_actor_\w+)\[.*?\]\((.*?)\)\s*$", pony, re.S | re.M))
+    hdr = open(HEADER).read()
+    protos = dict(re.findall(r"GPU_ACTOR_API\s+[\w\s\*]+?\b(gpu_actor_\w+)\s*\((.*?)\);", hdr, re.S))
+    host_only = {"gpu_actor_set_transport", "gpu_actor_stream", "gpu_actor_last_drain_ms"}
+    assert set(decl) <= set(protos)
+    assert set(protos) - set(decl) == host_only
+    for name, args in decl.items():
+        assert _arity(args) == _arity(protos[name]), name
