@@ -26,6 +26,25 @@
 
 using namespace gpa;
 
+// gups Updater tables (gups_basic/main.pony:145-155: table[k] = k + index*size),
+// one thread per word (field-major state[k * lcount + li]).
+__global__ void __launch_bounds__(kBlock) k_construct_table(uint32_t t, uint32_t n_live)
+{
+  const TypeDev& T = c_types[t];
+  const uint64_t n = T.lcount;
+  const uint64_t size = T.params[0] < T.words ? T.params[0] : T.words;
+  const uint64_t total = size * n;
+  for(uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
+      x += (uint64_t)gridDim.x * kBlock)
+  {
+    const uint64_t k = x / n, li = x - k * n;
+    if(li >= n_live) continue;
+    const uint64_t L = T.lfirst + li;
+    const uint64_t i = L * c_eng.nranks + c_eng.rank - T.first;
+    T.state[x] = k + i * size;
+  }
+}
+
 // pony_create's constructor run: initial state of a freshly created type.
 __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t, uint32_t n_live)
 {
@@ -61,11 +80,8 @@ __global__ void __launch_bounds__(kBlock) k_construct(uint32_t t, uint32_t n_liv
     case GPU_ACTOR_HT_GUPS_STREAMER:
       st[li] = polyrand_seeded(T.params[5] * i);
       break;
-    case GPU_ACTOR_HT_GUPS_UPDATER: {
-      const uint64_t size = T.params[0];
-      for(uint64_t k = 0; k < size && k < T.words; ++k) st[k * n + li] = k + i * size;
+    case GPU_ACTOR_HT_GUPS_UPDATER:      // the table: k_construct_table
       break;
-    }
     case GPU_ACTOR_HT_FIFO_SRC: {
       const uint64_t ns = T.params[1] ? T.params[1] : 1;
       st[li] = T.params[0] + i % ns;
@@ -917,6 +933,9 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   if(rc) return rc;
   hipLaunchKernelGGL(k_construct, dim3(blocks_for(live)), dim3(kBlock), 0, g.stream,
     type_id, (uint32_t)std::min<uint64_t>(live, t.lcount));
+  if(t.ht == GPU_ACTOR_HT_GUPS_UPDATER)
+    hipLaunchKernelGGL(k_construct_table, dim3(4096), dim3(kBlock), 0, g.stream,
+      type_id, (uint32_t)std::min<uint64_t>(live, t.lcount));
   HIPCK(hipGetLastError());
   const unsigned long long live_ull = live;
   HIPCK(hipMemcpyAsync(g.d_live + type_id, &live_ull, sizeof(live_ull), hipMemcpyHostToDevice,

@@ -4,7 +4,11 @@ only, as the task contract asks; this reports the others for DESIGN.md).
 Each workload is built with ponyc_amd.workloads at its BASELINE size and run
 to quiescence with gpu_actor_run; rate = delivered messages / wall time of the
 run (host sends done before the clock starts). One JSON line per config.
-usage: python scripts/bench_configs.py [names...]
+With --cpu, the reference runtime (oracle/_ref/harness_*, libponyrt built
+from the reference sources) runs the same config on the host's cores
+(--ponymaxthreads=min(16, cores) --ponynoblock --ponynoscale) and its rate is
+reported beside the GPU's ("cpu_ref").
+usage: python scripts/bench_configs.py [--cpu] [names...]
 """
 import json
 import os
@@ -27,13 +31,46 @@ CONFIGS = {
     "c3_fanin": (lambda e: W.fanin(e, 100_000, 4, 100, 0), {}),
     # C4: gups_basic, 2^24 table over 8 updaters, 64 streamers x 1024 x 100
     "c4_gups": (lambda e: W.gups(e, 24, 8, 64, 1024, 100), {}),
+    # C4 at GPU width (2^30-word table as 8 shards): the
+    # reference's --streamers option raised from 4 to 1,048,576 (each a
+    # sequential PolyRand stream; 512 zones fill the GPU), --chunk 16,
+    # --iterate 8: 151M updates. Ceiling for the access pattern: random 64-bit
+    # atomicXor over 2^30 words, 17.75 G/s (scripts/ubench_gups.hip)
+    "c4_gups_wide": (lambda e: W.gups(e, 30, 8, 1 << 20, 16, 8), {}),
     # C5, one GPU's share: 8M actors, token ring + 4 random pings each, 16 hops
     "c5_storm_8m": (lambda e: W.storm(e, 8 * M, 4, 16), {}),
 }
 
 
+# reference harness + arguments for the configs it runs (oracle/harness/*.c)
+CPU_REF = {
+    "c1_ring": ("ring", {"size": 1000, "count": 100, "pass": 10000}),
+    "c3_fanin": ("fanin", {"senders": 100_000, "analyzers": 4, "msgs": 100, "seedmode": 0}),
+    "c4_gups": ("gups", {"logtable": 24, "updaters": 8, "streamers": 64, "chunk": 1024,
+                         "iterate": 100, "batched": 0}),
+}
+
+
+def cpu_ref(name):
+    if name not in CPU_REF:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    harness, args = CPU_REF[name]
+    threads = max(1, min(16, os.cpu_count() or 1))
+    try:
+        info, _ = pyoracle.run_harness(harness, dict(args, threads=threads, noscale=1), None,
+                                       timeout=120)
+    except Exception as exc:            # report, never fake
+        return {"error": repr(exc)[:200]}
+    return {"msgs_per_s": round(info["msgs_per_sec"], 1), "msgs": info["msgs"],
+            "seconds": round(info["seconds"], 3), "threads": threads}
+
+
 def main():
-    names = sys.argv[1:] or list(CONFIGS)
+    args = sys.argv[1:]
+    with_cpu = "--cpu" in args
+    names = [a for a in args if a != "--cpu"] or list(CONFIGS)
     for name in names:
         setup, kw = CONFIGS[name]
         e = Engine(**kw)
@@ -47,7 +84,8 @@ def main():
         e.shutdown()
         print(json.dumps({"config": name, "steps": steps, "delivered": c["delivered"],
                           "seconds": round(secs, 4), "msgs_per_s": round(c["delivered"] / secs, 1),
-                          "dropped": c["dropped"]}), flush=True)
+                          "dropped": c["dropped"],
+                          "cpu_ref": cpu_ref(name) if with_cpu else None}), flush=True)
 
 
 if __name__ == "__main__":
