@@ -46,7 +46,10 @@ extern "C" {
 #define GPU_ACTOR_EMAILBOX     -4   /* a mailbox overflowed; messages dropped  */
 #define GPU_ACTOR_EHIP         -5   /* HIP runtime error                       */
 #define GPU_ACTOR_ESTATE       -6   /* not initialised / already initialised   */
-#define GPU_ACTOR_ERANGE       -7   /* sequence or id space exhausted          */
+#define GPU_ACTOR_ERANGE       -7   /* sequence or id space exhausted: more than
+                                       65,534 sends by one actor in one superstep
+                                       (16,382 with n_ranks > 1), or more than
+                                       2^23 actors on one rank                  */
 #define GPU_ACTOR_ECOMM        -8   /* RCCL / exchange failure                 */
 #define GPU_ACTOR_EBUSY        -9   /* an asynchronous run is in flight         */
 

@@ -313,6 +313,7 @@ int upload_types()
   e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
+  e.seq_max = R() > 1 ? kXSeqMax : kSeqMax;
   e.dbg = g.d_dbg;
   e.spawn_key = g.d_skey[0]; e.spawn_arg = g.d_sarg[0];
   e.spawn_n = g.d_spawn_n; e.spawn_cap = g.spawn_cap;
@@ -460,6 +461,10 @@ int exchange_host(uint64_t& total)
   if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
   if(roff)
     HIPCK(hipMemcpyAsync(g.d_xin, g.h_xin, roff * sizeof(XRec), hipMemcpyHostToDevice, g.stream));
+  // per-peer counts for k_xinject (the sender's rank of each record)
+  for(uint32_t p = 0; p < n; ++p) g.h_xrecv[p] = rc[p];
+  HIPCK(hipMemcpyAsync(g.d_xrecv, g.h_xrecv.data(), n * sizeof(unsigned long long),
+    hipMemcpyHostToDevice, g.stream));
   total = roff;
   return 0;
 }
@@ -505,7 +510,7 @@ int exchange(uint32_t land_par)
   if(total)
   {
     hipLaunchKernelGGL(k_xinject, dim3(blocks_for(total, kLandRecs)), dim3(kLandThreads), 0, g.stream,
-      (const XRec*)g.d_xin, total, land_par);
+      (const XRec*)g.d_xin, total, land_par, (const unsigned long long*)g.d_xrecv);
     HIPCK(hipGetLastError());
   }
   HIPCK(hipMemsetAsync(g.d_xcount, 0, n * sizeof(unsigned long long), g.stream));

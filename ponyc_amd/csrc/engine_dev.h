@@ -62,13 +62,21 @@ struct ORec {            // outbox record (zone scratch), 16 B
   uint64_t arg;
 };
 
-struct XRec {            // cross-rank record, 24 B
-  uint32_t to;
-  uint32_t w;            // seq << 16 | beh << 12 (seq == kSeqApply: reducible)
-  uint32_t from;
-  uint32_t pad;
+// Cross-rank record, 16 B: ids travel as local slots (the receiver is the
+// owner of `to`; the sender's rank is known from which peer's segment the
+// record arrived in), which leaves 14 bits for the sender's sequence number:
+//   w0 = seq >> 9 << 27 | beh << 23 | to_local   (to_local < 2^23 = kMaxZones * kZone)
+//   w1 = (seq & 511) << 23 | from_local
+// seq == kXSeqApply marks a reducible apply. Per-step sends per actor are
+// therefore limited to kXSeqMax when n_ranks > 1 (kSeqMax otherwise).
+struct XRec {
+  uint32_t w0;
+  uint32_t w1;
   uint64_t arg;
 };
+constexpr uint32_t kXSeqApply = 0x3FFFu;
+constexpr uint32_t kXSeqMax = 0x3FFEu;
+static_assert(sizeof(XRec) == 16, "XRec is 16 B");
 
 __device__ __forceinline__ uint64_t zkey(const ZRec& r)
 {
@@ -100,7 +108,8 @@ struct EngDev {
   unsigned long long* pend;       // per-step pending counters
   XRec*  xout;                    // [nranks][xcap]
   unsigned long long* xcount;     // [nranks]
-  uint32_t xcap, pad1;
+  uint32_t xcap;
+  uint32_t seq_max;               // kSeqMax, or kXSeqMax with n_ranks > 1
   unsigned long long* dbg;        // [n_zones][8] phase stamps (diagnostic build)
   // actors created by behaviours this step (gpu_actor_type_reserve): sort key
   // type << 52 | creator << 20 | seq << 4 | beh, and the constructor's arg
@@ -156,6 +165,17 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t to)
     if(owner != c_eng.rank) return c_eng.n_zones + owner;
   }
   return rdiv(to) >> kZoneBits;
+}
+
+// Cross-rank record from global ids and a (seq << 16 | beh << 12) word.
+__device__ __forceinline__ XRec xpack(uint32_t to, uint32_t w, uint32_t from, uint64_t arg)
+{
+  const uint32_t seq = (w >> 16) == kSeqApply ? kXSeqApply : (w >> 16);
+  XRec x;
+  x.w0 = (seq >> 9) << 27 | ((w >> 12) & 0xFu) << 23 | rdiv(to);
+  x.w1 = (seq & 0x1FFu) << 23 | rdiv(from);
+  x.arg = arg;
+  return x;
 }
 
 // Per-lane bookkeeping while one actor drains.
@@ -239,8 +259,7 @@ __device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint
     const unsigned long long pos = atomicAdd(&c_eng.xcount[b - nz], 1ull);
     if(pos < c_eng.xcap)
     {
-      XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
-      x->to = to; x->w = w; x->from = a.self; x->pad = 0; x->arg = arg;
+      c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] = xpack(to, w, a.self, arg);
     }
     else
       atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], 1ull);
@@ -266,7 +285,7 @@ __device__ __forceinline__ void outbox_put(ActorCtx& a, uint32_t to, uint32_t w,
 __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t beh, uint64_t arg)
 {
   a.sent++;
-  if(a.seq >= kSeqMax)
+  if(a.seq >= c_eng.seq_max)
   {
     atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
     return;
@@ -282,7 +301,7 @@ __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t b
 __device__ __forceinline__ void spawn_actor(ActorCtx& a, uint32_t type, uint32_t beh, uint64_t arg)
 {
   a.sent++;
-  if(a.seq >= kSeqMax)
+  if(a.seq >= c_eng.seq_max)
   {
     atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
     return;

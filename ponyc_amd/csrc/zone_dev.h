@@ -707,9 +707,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       {
         if(pos < c_eng.xcap)
         {
-          XRec* x = c_eng.xout + (size_t)(b - nz) * c_eng.xcap + pos;
-          x->to = r.x; x->w = r.y & ~kZoneMask; x->from = from; x->pad = 0;
-          x->arg = ((uint64_t)r.w << 32) | r.z;
+          c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] =
+            xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z);
         }
         else
           ++xover;
@@ -858,13 +857,27 @@ __global__ void __launch_bounds__(kLandThreads) k_inject(const gpu_msg_t* msgs, 
   land_records(r, cur, s_hist, s_base);
 }
 
-// Records received from other ranks.
-__global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64_t n, uint32_t cur)
+// Records received from other ranks: `in` holds each peer's records in rank
+// order, rcnt[p] of them from peer p (clipped to xcap); the sender's rank of a
+// record is the segment it lies in.
+__global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64_t n, uint32_t cur,
+  const unsigned long long* rcnt)
 {
   __shared__ uint32_t s_hist[kMaxZones];
   __shared__ uint32_t s_base[kMaxZones];
   __shared__ unsigned long long s_app[GPU_ACTOR_MAX_TYPES];
+  __shared__ unsigned long long s_roff[kMaxRanks];
+  const uint32_t R = c_eng.nranks, me = c_eng.rank;
   if(threadIdx.x < GPU_ACTOR_MAX_TYPES) s_app[threadIdx.x] = 0;
+  if(threadIdx.x == 0)
+  {
+    unsigned long long acc = 0;
+    for(uint32_t p = 0; p < R; ++p)
+    {
+      s_roff[p] = acc;
+      acc += min(rcnt[p], (unsigned long long)c_eng.xcap);
+    }
+  }
   __syncthreads();
   LandRec r[kLandPer];
 #pragma unroll
@@ -875,16 +888,25 @@ __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64
     if(i < n)
     {
       const XRec x = in[i];
-      if((x.w >> 16) == kSeqApply)
+      uint32_t src = 0;
+      for(uint32_t p = 1; p < R; ++p)
+        if(i >= s_roff[p]) src = p;
+      const uint32_t seq = (x.w0 >> 27) << 9 | (x.w1 >> 23);
+      const uint32_t beh = (x.w0 >> 23) & 0xFu;
+      const uint32_t to = (x.w0 & 0x7FFFFFu) * R + me;
+      if(seq == kXSeqApply)
       {
-        reducible_apply_local(x.to, (x.w >> 12) & 0xFu, x.arg);
-        const int t = type_of_global(x.to);
+        reducible_apply_local(to, beh, x.arg);
+        const int t = type_of_global(to);
         if(t >= 0) atomicAdd(&s_app[t], 1ull);
       }
       else
       {
         r[u].valid = true;
-        r[u].to = x.to; r[u].w = x.w; r[u].from = x.from; r[u].arg = x.arg;
+        r[u].to = to;
+        r[u].w = seq << 16 | beh << 12;
+        r[u].from = (x.w1 & 0x7FFFFFu) * R + src;
+        r[u].arg = x.arg;
       }
     }
   }

@@ -1,7 +1,7 @@
 """CPU (gloo, world_size 2+) checks of the multi-rank host plumbing, launched by
 tests/test_multirank.py: the ctypes callbacks the C library calls for its
 host-staged exchange (exactly as engine.hip's exchange_host drives them: a
-counts all-to-all, then a ragged byte all-to-all of 24-B records), the
+counts all-to-all, then a ragged byte all-to-all of 16-B records), the
 counter all-reduce, and gather_state's reassembly of the id % R partition."""
 import ctypes
 import os
@@ -16,7 +16,7 @@ import torch.distributed as dist         # noqa: E402
 from ponyc_amd.dist import GlooTransport, gather_state   # noqa: E402
 from ponyc_amd.engine import _wrap_transport             # noqa: E402
 
-XREC = 24
+XREC = 16
 
 
 class FakeEngine:
