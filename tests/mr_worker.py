@@ -28,6 +28,9 @@ CASES = {
     "gups": (lambda e: W.gups(e, 14, 8, 64, 64, 3), W.gups_result, {}),
     "storm": (lambda e: W.storm(e, 3000, 4, 12), lambda e, w: e.state_read(w["type"]), {}),
     "fifo": (lambda e: W.fifo(e, 64, 7, 10, 4, batch=7, mailbox_cap=1024), W.fifo_result, {}),
+    # 600 sends per source per step: sequence numbers past 511 use the high
+    # bits of the 16-B cross-rank record's 14-bit seq (engine_dev.h XRec)
+    "fifo_seq": (lambda e: W.fifo(e, 4, 3, 1, 600, mailbox_cap=2048), W.fifo_result, {}),
 }
 
 

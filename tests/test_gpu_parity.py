@@ -79,14 +79,16 @@ def test_storm(engine_factory, oracle):
     _assert_same(g, o)
 
 
-@pytest.mark.parametrize("sources,sinks,bursts,m,batch", [(64, 8, 10, 4, 0), (40, 5, 6, 3, 7),
-                                                          (16, 2, 5, 9, 4)])
-def test_fifo_order_exact(engine_factory, oracle, sources, sinks, bursts, m, batch):
+@pytest.mark.parametrize("sources,sinks,bursts,m,batch,cap", [(64, 8, 10, 4, 0, 1024),
+                                                              (40, 5, 6, 3, 7, 1024),
+                                                              (16, 2, 5, 9, 4, 1024),
+                                                              (4, 2, 1, 600, 0, 2048)])
+def test_fifo_order_exact(engine_factory, oracle, sources, sinks, bursts, m, batch, cap):
     """Order-sensitive fold: equal only if delivery order is exactly the
     canonical (sender, seq) order, including carry-over under a batch limit."""
     # a batch limit below the arrival rate builds a backlog: size the rings for it
     g, o = _both(engine_factory, oracle,
-                 lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=1024),
+                 lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=cap),
                  W.fifo_result)
     _assert_same(g, o)
     assert g[2][2].sum() == 0          # no per-pair FIFO violations
