@@ -125,12 +125,29 @@ def cpu_baseline(args) -> dict | None:
     except Exception as exc:       # report, never fake
         return {"value": None, "unit": "msgs/s", "cores": threads, "kind": "reference",
                 "sample": f"failed: {exc!r}"}
+    # also the single-thread rate (smaller budget: ~5 s at 1.9 M msgs/s)
+    one = None
+    try:
+        info1, _ = pyoracle.run_harness("ubench", dict(sample, threads=1, budget=4), None,
+                                        timeout=120)
+        one = round(info1["msgs_per_sec"], 1)
+    except Exception:
+        one = None
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                         None)
+    except OSError:
+        pass
     return {"value": round(info["msgs_per_sec"], 1), "unit": "msgs/s", "cores": threads,
+            "value_1thread": one, "cpu_model": model,
             "kind": "reference",
             "sample": (f"harness_ubench on KittyMac/ponyc libponyrt (-O3, pthread scaling), "
                        f"{args.actors} pingers x {args.initial} initial pings, forward budget "
                        f"{args.cpu_budget} ({info['msgs']} msgs, {info['seconds']:.2f} s), "
-                       f"--ponymaxthreads={threads} --ponynoblock --ponynoscale")}
+                       f"--ponymaxthreads={threads} --ponynoblock --ponynoscale; value_1thread: "
+                       f"--ponymaxthreads=1, forward budget 4")}
 
 
 def main():
