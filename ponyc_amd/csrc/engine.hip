@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -184,7 +185,7 @@ struct Engine {
   std::mutex mu;
   // asynchronous run (gpu_actor_run_async): one progress thread at a time
   std::thread worker;
-  bool async_busy = false;
+  std::atomic<bool> async_busy{false};   // read without the lock
   int async_rc = 0;
   uint64_t async_steps = 0;
   bool init = false;
@@ -1069,6 +1070,7 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
 
 GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
 {
+  if(g.async_busy) return GPU_ACTOR_EBUSY;     // without waiting for the lock it holds
   std::lock_guard<std::mutex> lk(g.mu);
   if(g.async_busy) return GPU_ACTOR_EBUSY;
   return run_locked(max_steps, steps_done);
@@ -1076,6 +1078,7 @@ GPU_ACTOR_API int gpu_actor_run(uint64_t max_steps, uint64_t* steps_done)
 
 GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done, void* ctx)
 {
+  if(g.async_busy) return GPU_ACTOR_EBUSY;
   {
     std::lock_guard<std::mutex> lk(g.mu);
     if(!g.init) return GPU_ACTOR_ESTATE;
@@ -1124,7 +1127,6 @@ GPU_ACTOR_API int gpu_actor_wait(uint64_t* steps_done)
 
 GPU_ACTOR_API int gpu_actor_busy(void)
 {
-  std::lock_guard<std::mutex> lk(g.mu);
   return g.async_busy ? 1 : 0;
 }
 

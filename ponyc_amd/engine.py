@@ -35,7 +35,7 @@ NONE_ID = 0xFFFFFFFFFFFFFFFF
 
 ERRORS = {
     -1: "EINVAL", -2: "ENOMEM", -3: "ENODEV", -4: "EMAILBOX", -5: "EHIP",
-    -6: "ESTATE", -7: "ERANGE", -8: "ECOMM",
+    -6: "ESTATE", -7: "ERANGE", -8: "ECOMM", -9: "EBUSY",
 }
 
 
