@@ -375,6 +375,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // ---- 1. count --------------------------------------------------------------
   const uint32_t nc = min(c_eng.carry_n[cur][z], cap);
   const uint32_t nl = min(c_eng.land_n[cur][z], cap);
+  if(nc + nl == 0)
+  {
+    // an idle zone (uniform: every thread read the same counters) has
+    // nothing to count, run or send — the quiet tail of a run, or zones of
+    // a sparse workload
+    if(tid == 0) c_eng.carry_n[nxt][z] = 0;
+    return;
+  }
   const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
   const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
   const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
