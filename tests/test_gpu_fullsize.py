@@ -99,3 +99,22 @@ def test_c5_storm_8m(engine_factory):
     for h in range(hops + 1):
         ping_all ^= ox ^ (h if (n * r) % 2 else 0)
     assert int(np.bitwise_xor.reduce(st[1])) == tok_all ^ ping_all
+
+
+def test_c1_ring_full(engine_factory):
+    """C1 at its full size (examples/ring --size 1000 --count 100 --pass 10000):
+    the reference's own totals — 1,000,100 `pass` messages, 11 received by the
+    first actor of each ring and 10 by every other one, and pass(0) reached
+    exactly one actor per ring (the reference harness reproduces these at
+    1/2/4/8 scheduler threads)."""
+    e = engine_factory()
+    w = W.ring(e, 1000, 100, 10000)
+    steps = e.run()
+    c = e.counts()
+    recv, done = W.ring_result(e, w)
+    assert c["dropped"] == 0 and c["pending"] == 0
+    assert c["delivered"] == 1_000_100 + 100           # + one set per ring
+    assert steps == 10_001
+    per_ring = recv.reshape(100, 1000)
+    assert (per_ring[:, 0] == 11).all() and (per_ring[:, 1:] == 10).all()
+    assert int(done.sum()) == 100 and (done.reshape(100, 1000).sum(axis=1) == 1).all()
