@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PINGER_STATE_BYTES = 24        # rng x, y + count
 # PMC summary (scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of the current k_step build
-PMC_TAG = "r01g"
+PMC_TAG = "r01i"
 REC_BYTES = 16
 MAILBOX_BYTES = 8              # mailbox head/tail per active actor (SURVEY §8 d3's M)
 # device atomic peak measured on MI355X by scripts/ubench_mem.hip (random u32
