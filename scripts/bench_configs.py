@@ -25,6 +25,8 @@ M = 1 << 20
 CONFIGS = {
     # C1: examples/ring --size 1000 --count 100 --pass 10000 (the CPU plumbing case)
     "c1_ring": (lambda e: W.ring(e, 1000, 100, 10000), {}),
+    # C1 as one ring (--count 1): a one-zone world, one k_step_run launch per 256 steps
+    "c1_ring_one": (lambda e: W.ring(e, 1000, 1, 10000), {}),
     # C2, deterministic form (budgeted): 1M pingers x 5 tokens x 32 hops
     "c2_ubench_det": (lambda e: W.ubench(e, M, 5, det=True, hops=32), {}),
     # C3: fan-in, 100K senders -> 4 analyzers x 100 messages
@@ -45,6 +47,7 @@ CONFIGS = {
 # reference harness + arguments for the configs it runs (oracle/harness/*.c)
 CPU_REF = {
     "c1_ring": ("ring", {"size": 1000, "count": 100, "pass": 10000}),
+    "c1_ring_one": ("ring", {"size": 1000, "count": 1, "pass": 10000}),
     "c3_fanin": ("fanin", {"senders": 100_000, "analyzers": 4, "msgs": 100, "seedmode": 0}),
     "c4_gups": ("gups", {"logtable": 24, "updaters": 8, "streamers": 64, "chunk": 1024,
                          "iterate": 100, "batched": 0}),
