@@ -660,6 +660,47 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t nout = min(s_nout, cap);
   const ORec* Oz = c_eng.O + c_eng.zoff[z];
   uint32_t dropped = 0, xover = 0;
+  // r = {to, w, arg lo, arg hi} -> position pos of bucket b's chunk
+  auto emit = [&](const uint4& r, uint32_t b, uint32_t pos) __attribute__((always_inline)) {
+    const uint32_t from = (L0 + (r.y & kZoneMask)) * R + me;
+    if(b < nz)
+    {
+      if(pos < zone_capacity(b))
+      {
+        uint4 v;
+        v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
+        v.y = from;
+        v.z = r.z;
+        v.w = r.w;
+        st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
+      }
+      else
+        ++dropped;
+    }
+    else
+    {
+      if(pos < c_eng.xcap)
+      {
+        c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] =
+          xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z);
+      }
+      else
+        ++xover;
+    }
+  };
+  if(nout <= kZoneThreads)
+  {
+    // a sparse step (at most one record per thread): rank each record in its
+    // bucket and store it straight away — the tile sort only groups stores
+    // into runs, and a chunk's order is free (receivers order by key)
+    if(tid < nout)
+    {
+      const uint4 r = ld16(reinterpret_cast<const uint4*>(Oz + tid));
+      const uint32_t b = bucket_of(r.x);
+      emit(r, b, s_base[b] + atomicAdd(&s_tcnt[b], 1u));
+    }
+  }
+  else
   for(uint32_t t0 = 0; t0 < nout; t0 += kTile)
   {
     const uint32_t m = min(kTile, nout - t0);
@@ -692,35 +733,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     __syncthreads();
     for(uint32_t p = tid; p < m; p += kZoneThreads)
     {
-      // r = {to, w, arg lo, arg hi}
       const uint4 r = s_pool[p];
       const uint32_t b = bucket_of(r.x);
-      const uint32_t pos = s_base[b] + (p - s_tst[b]);
-      const uint32_t from = (L0 + (r.y & kZoneMask)) * R + me;
-      if(b < nz)
-      {
-        if(pos < zone_capacity(b))
-        {
-          uint4 v;
-          v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
-          v.y = from;
-          v.z = r.z;
-          v.w = r.w;
-          st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
-        }
-        else
-          ++dropped;
-      }
-      else
-      {
-        if(pos < c_eng.xcap)
-        {
-          c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] =
-            xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z);
-        }
-        else
-          ++xover;
-      }
+      emit(r, b, s_base[b] + (p - s_tst[b]));
     }
     __syncthreads();
     for(uint32_t b = tid; b < nb; b += kZoneThreads)
