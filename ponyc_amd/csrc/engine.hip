@@ -186,6 +186,7 @@ struct Engine {
   // asynchronous run (gpu_actor_run_async): one progress thread at a time
   std::thread worker;
   std::atomic<bool> async_busy{false};   // read without the lock
+  std::atomic<bool> async_started{false};  // the progress thread holds mu
   int async_rc = 0;
   uint64_t async_steps = 0;
   bool init = false;
@@ -1085,9 +1086,11 @@ GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done
     if(g.async_busy) return GPU_ACTOR_EBUSY;
   }
   join_worker();                      // reap the previous, finished run
+  {
   std::lock_guard<std::mutex> lk(g.mu);
   if(g.async_busy) return GPU_ACTOR_EBUSY;
   g.async_busy = true;
+  g.async_started = false;
   g.async_rc = 0;
   g.async_steps = 0;
   const int dev = g.device;
@@ -1098,6 +1101,7 @@ GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done
       uint64_t steps = 0;
       {
         std::lock_guard<std::mutex> wl(g.mu);
+        g.async_started = true;
         rc = hipSetDevice(dev) == hipSuccess ? run_locked(max_steps, &steps) : GPU_ACTOR_EHIP;
         g.async_rc = rc;
         g.async_steps = steps;
@@ -1112,6 +1116,10 @@ GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done
     g.async_busy = false;
     return GPU_ACTOR_ENOMEM;
   }
+  }
+  // return only once the progress thread holds the lock, so every later call
+  // on this library is serialised behind the run it started
+  while(!g.async_started) std::this_thread::yield();
   return 0;
 }
 

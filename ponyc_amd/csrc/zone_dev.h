@@ -105,6 +105,50 @@ __device__ uint32_t block_scan_zone(uint32_t* arr, uint32_t* s_tmp)
   return total;
 }
 
+// Phase-1 scans in one pass: off = exclusive scan of cnt + ccnt (segment
+// starts), aux = exclusive scan of ccnt (carry starts). Two wave-level scans
+// share the barriers, and waves 0 and 1 scan the two wave-total vectors side by
+// side. s_tmp2 holds 2 * kZoneWaves entries. All threads call it; it ends
+// behind a barrier.
+__device__ void block_scan_zone_pair(const uint32_t* cnt, const uint32_t* ccnt, uint32_t* off,
+                                     uint32_t* aux, uint32_t* s_tmp2)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  static_assert(kZoneWaves >= 2 && kZoneWaves <= 64, "pair scan: one wave per vector");
+  constexpr uint32_t per = kZone / kZoneThreads;
+  uint32_t va[per], vb[per];
+  uint32_t sa = 0, sb = 0;
+#pragma unroll
+  for(uint32_t k = 0; k < per; ++k)
+  {
+    vb[k] = ccnt[tid * per + k];
+    va[k] = cnt[tid * per + k] + vb[k];
+    sa += va[k];
+    sb += vb[k];
+  }
+  const uint32_t ia = wave_incl_scan(sa, lane);
+  const uint32_t ib = wave_incl_scan(sb, lane);
+  if(lane == 63) { s_tmp2[wv] = ia; s_tmp2[kZoneWaves + wv] = ib; }
+  __syncthreads();
+  if(wv < 2)
+  {
+    uint32_t* t = s_tmp2 + wv * kZoneWaves;
+    uint32_t x = lane < (uint32_t)kZoneWaves ? t[lane] : 0u;
+    x = wave_incl_scan(x, lane);
+    if(lane < (uint32_t)kZoneWaves) t[lane] = x;
+  }
+  __syncthreads();
+  uint32_t ra = (wv ? s_tmp2[wv - 1] : 0u) + ia - sa;
+  uint32_t rb = (wv ? s_tmp2[kZoneWaves + wv - 1] : 0u) + ib - sb;
+#pragma unroll
+  for(uint32_t k = 0; k < per; ++k)
+  {
+    off[tid * per + k] = ra; ra += va[k];
+    aux[tid * per + k] = rb; rb += vb[k];
+  }
+  __syncthreads();
+}
+
 // Exclusive scan of in[0, n) into out[0, n) (LDS) by a kZoneThreads workgroup,
 // each thread taking a contiguous run; returns the total. All threads call it;
 // it ends behind a barrier.
@@ -345,6 +389,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   uint16_t* const s_idx = reinterpret_cast<uint16_t*>(s_aux + kZone);  // index into carry ++ landing
   extern __shared__ uint32_t s_dyn[];   // [nb] histogram, [nb] chunk bases, [nb] tile counts, [nb] tile starts
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
+  __shared__ uint32_t s_tmp2[2 * kZoneWaves];
   __shared__ uint32_t s_nout;
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
@@ -432,10 +477,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.carry_n[cur][z] = 0;
     c_eng.land_n[cur][z] = 0;
   }
-  for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_off[i] = s_cnt[i] + s_ccnt[i]; s_aux[i] = s_ccnt[i]; }
-  __syncthreads();
-  (void)block_scan_zone(s_off, s_tmp);
-  (void)block_scan_zone(s_aux, s_tmp);
+  block_scan_zone_pair(s_cnt, s_ccnt, s_off, s_aux, s_tmp2);
   GPA_STAMP(2);
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
