@@ -544,6 +544,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   // carry-out sizes (known before any handler runs) -> offsets
   const uint32_t zbatch = tz >= 0 ? c_types[tz].batch : 0u;
+  int any_rem = 0;
   for(uint32_t i = tid; i < kZone; i += kZoneThreads)
   {
     uint32_t rem = 0;
@@ -559,9 +560,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       rem = n > bt ? n - bt : 0u;
     }
     s_aux[i] = rem;
+    any_rem |= rem != 0u;
   }
-  __syncthreads();
-  const uint32_t ncout = block_scan_zone(s_aux, s_tmp);
+  // no actor over its batch (the usual step): s_aux is all zeros, which is
+  // already its own exclusive scan
+  const uint32_t ncout = __syncthreads_or(any_rem) ? block_scan_zone(s_aux, s_tmp) : 0u;
   if(tid == 0)
     c_eng.carry_n[nxt][z] = min(ncout, cap);
 
