@@ -72,7 +72,7 @@ typedef struct gpu_actor_config_t
   uint32_t n_ranks;         /* processes (one per GPU) sharing the actor space   */
   uint32_t rank;            /* this process's rank, 0 <= rank < n_ranks          */
   uint32_t batch;           /* default per-step drain limit (0 -> 100)           */
-  uint32_t mailbox_cap;     /* default mailbox ring capacity, power of 2 (0->64) */
+  uint32_t mailbox_cap;     /* default mailbox ring capacity, power of 2 (0->16) */
   uint32_t max_exchange;    /* per-peer records per step for n_ranks>1 (0->auto) */
   uint64_t max_actors;      /* capacity of the global id space (0 -> 1<<26)      */
   const void* comm_id;      /* 128-byte ncclUniqueId from rank 0 (n_ranks > 1)  */
@@ -146,9 +146,17 @@ GPU_ACTOR_API int gpu_actor_type_live(uint32_t type_id, uint64_t* live);
 /* Host staging buffer for up to n messages, owned by the library and valid
  * until the next gpu_actor_alloc_msgs / gpu_actor_shutdown. */
 GPU_ACTOR_API int gpu_actor_alloc_msgs(uint64_t n, gpu_msg_t** buf);
-/* Send n messages in order (a chain). Ownership passes to the library. */
+/* Send n messages in order (a chain). Ownership passes to the library. With
+ * n_ranks > 1 every message must be addressed to an actor this rank owns
+ * (gpu_actor_owner(to) == rank): each rank injects its own share, and a
+ * message for another rank's actor fails the whole call with
+ * GPU_ACTOR_EINVAL before anything is sent. */
 GPU_ACTOR_API int gpu_actor_sendv(const gpu_msg_t* first, uint64_t n);
-/* pony_sendi (actor.c:959-968) analogue. */
+/* pony_sendi (actor.c:959-968) analogue. The message is appended to a host
+ * staging list (no device work, no synchronisation) and injected, in call
+ * order and before any later gpu_actor_sendv, by the next call that runs or
+ * observes the engine (run*, sync, state_*, counts). Same ownership rule as
+ * gpu_actor_sendv. */
 GPU_ACTOR_API int gpu_actor_send(uint64_t to, uint32_t behaviour, uint64_t arg);
 
 /* ---- running (the scheduler run loop, scheduler.c:953-1090) ------------- */

@@ -41,6 +41,7 @@ use @gpu_actor_counts[I32](out: GpuActorCounts tag)
 use @gpu_actor_owner[U32](id: U64)
 use @gpu_actor_strerror[Pointer[U8] val](code: I32)
 use @pony_register_thread[None]()
+use @pony_unregister_thread[None]()
 
 primitive HtRing fun apply(): U32 => 1            // examples/ring
 primitive HtPinger fun apply(): U32 => 2          // examples/message-ubench
@@ -114,6 +115,9 @@ primitive GpuRunDone
     @{(notify: GpuRunNotify, rc: I32, steps: U64) =>
       @pony_register_thread()
       notify.gpu_run_done(rc, steps)
+      // pair the registration (pony.h:520-536, as asio/epoll.c does): the
+      // library may run the next asynchronous run on a new thread
+      @pony_unregister_thread()
     }
 
 class GpuActors

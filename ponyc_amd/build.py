@@ -13,8 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "engine.hip")
-DEPS = [SRC] + [os.path.join(HERE, "csrc", f) for f in ("engine_dev.h", "rng_dev.h", "zone_dev.h")] \
-    + [os.path.join(ROOT, "include", "gpu_actor.h")]
+DEPS = [os.path.join(HERE, "csrc", f) for f in sorted(os.listdir(os.path.join(HERE, "csrc")))
+        if f.endswith((".hip", ".h"))] + [os.path.join(ROOT, "include", "gpu_actor.h")]
 OUT = os.path.join(HERE, "libgpuactor.so")
 OUT_STAMPS = os.path.join(HERE, "libgpuactor_stamps.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -24,6 +24,7 @@
 
 #include "engine_dev.h"
 #include "zone_dev.h"
+#include "sparse_dev.h"
 
 using namespace gpa;
 
@@ -183,7 +184,9 @@ struct HostType {
 
 struct Engine {
   std::mutex mu;
-  // asynchronous run (gpu_actor_run_async): one progress thread at a time
+  // asynchronous run (gpu_actor_run_async): one progress thread at a time;
+  // wmu guards the thread object (joined or detached by whoever reaps it)
+  std::mutex wmu;
   std::thread worker;
   std::atomic<bool> async_busy{false};   // read without the lock
   std::atomic<bool> async_started{false};  // the progress thread holds mu
@@ -213,6 +216,9 @@ struct Engine {
   unsigned long long* d_pend = nullptr;
   unsigned long long* d_dbg = nullptr;   // phase stamps of the diagnostic build
   gpu_msg_t* h_msgs = nullptr; uint64_t h_msgs_cap = 0;
+  // gpu_actor_send appends here; flushed (one H2D + k_inject) before the
+  // next operation that observes device state, so a send costs no sync
+  std::vector<gpu_msg_t> deferred;
   gpu_msg_t* d_msgs = nullptr; uint64_t d_msgs_cap = 0;
   uint64_t host_seq = 0;
   uint64_t steps_total = 0;
@@ -243,6 +249,10 @@ struct Engine {
   unsigned long long* d_live = nullptr;  // [GPU_ACTOR_MAX_TYPES] live actors per type
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  // small-step path (k_sparse)
+  SparseCtl* d_ctl = nullptr;
+  SparseCtl* h_ctl = nullptr;             // pinned
+  uint64_t sparse_launches = 0, sparse_steps = 0;
 };
 
 Engine g;
@@ -672,6 +682,8 @@ void free_all()
   if(g.d_tstart) (void)hipFree(g.d_tstart);
   if(g.d_tcnt) (void)hipFree(g.d_tcnt);
   if(g.d_live) (void)hipFree(g.d_live);
+  if(g.d_ctl) (void)hipFree(g.d_ctl);
+  if(g.h_ctl) (void)hipHostFree(g.h_ctl);
   if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
@@ -689,12 +701,15 @@ void free_all()
   if(g.stream) (void)hipStreamDestroy(g.stream);
 }
 
-int sendv_locked(const gpu_msg_t* first, uint64_t n)
+// A host send must name an actor of this rank (each rank injects its own
+// share; k_inject lands only local mail).
+inline bool host_msg_ok(const gpu_msg_t& m)
 {
-  if(n == 0) return 0;
-  if(!first) return GPU_ACTOR_EINVAL;
-  for(uint64_t i = 0; i < n; ++i)
-    if(first[i].to >= g.n_actors || first[i].behaviour > 0xF) return GPU_ACTOR_EINVAL;
+  return m.to < g.n_actors && m.behaviour <= 0xF && (R() == 1 || m.to % R() == rank());
+}
+
+int inject_locked(const gpu_msg_t* first, uint64_t n)
+{
   if(g.host_seq + n >= (1ull << 40)) return GPU_ACTOR_ERANGE;
   if(n > g.d_msgs_cap)
   {
@@ -713,6 +728,26 @@ int sendv_locked(const gpu_msg_t* first, uint64_t n)
   g.host_seq += n;
   HIPCK(hipStreamSynchronize(g.stream));    // the caller may reuse its buffer
   return 0;
+}
+
+// gpu_actor_send's deferred messages, injected in call order.
+int flush_sends()
+{
+  if(g.deferred.empty()) return 0;
+  const int rc = inject_locked(g.deferred.data(), g.deferred.size());
+  g.deferred.clear();
+  return rc;
+}
+
+int sendv_locked(const gpu_msg_t* first, uint64_t n)
+{
+  if(n == 0) return 0;
+  if(!first) return GPU_ACTOR_EINVAL;
+  for(uint64_t i = 0; i < n; ++i)
+    if(!host_msg_ok(first[i])) return GPU_ACTOR_EINVAL;
+  int rc = flush_sends();                   // earlier single sends go first
+  if(rc) return rc;
+  return inject_locked(first, n);
 }
 
 } // namespace
@@ -781,6 +816,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_tstart, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
   HIPCK(hipMalloc(&g.d_tcnt, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
   HIPCK(hipMalloc(&g.d_live, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long)));
+  HIPCK(hipMalloc(&g.d_ctl, sizeof(SparseCtl)));
+  HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
   HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
   if(R() > 1)
@@ -817,9 +854,23 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
 }
 
 // Joins a finished (or running) asynchronous run; caller must NOT hold g.mu.
+// Called on the progress thread itself (the completion callback chaining a
+// run_async, wait or shutdown), it detaches instead: the thread ends right
+// after its callback returns.
 void join_worker()
 {
-  if(g.worker.joinable()) g.worker.join();
+  std::thread t;
+  {
+    std::lock_guard<std::mutex> wl(g.wmu);
+    if(!g.worker.joinable()) return;
+    if(g.worker.get_id() == std::this_thread::get_id())
+    {
+      g.worker.detach();
+      return;
+    }
+    t = std::move(g.worker);
+  }
+  t.join();
 }
 
 GPU_ACTOR_API int gpu_actor_shutdown(void)
@@ -840,10 +891,12 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
+  g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
   g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;
   for(int p = 0; p < 2; ++p) g.d_skey[p] = g.d_sarg[p] = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
+  g.deferred.clear();
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
   g.h_xout = g.h_xin = nullptr;
@@ -1021,16 +1074,47 @@ GPU_ACTOR_API int gpu_actor_send(uint64_t to, uint32_t behaviour, uint64_t arg)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
-  if(to >= g.n_actors) return GPU_ACTOR_EINVAL;
   gpu_msg_t m;
   m.to = (uint32_t)to; m.behaviour = behaviour; m.arg = arg;
-  return sendv_locked(&m, 1);
+  if(to >= g.n_actors || !host_msg_ok(m)) return GPU_ACTOR_EINVAL;
+  if(g.host_seq + g.deferred.size() + 1 >= (1ull << 40)) return GPU_ACTOR_ERANGE;
+  try { g.deferred.push_back(m); } catch(...) { return GPU_ACTOR_ENOMEM; }
+  return 0;
+}
+
+// The small-step path applies to one rank without spawning types (spawned
+// ids are numbered by the host after each dense step). GPA_NO_SPARSE=1 turns
+// it off (A/B runs).
+bool sparse_ok()
+{
+  const char* e = getenv("GPA_NO_SPARSE");
+  return !(e && atoi(e) != 0) && R() == 1 && g.spawn_cap == 0 && g.n_zones > 0;
+}
+
+// One k_sparse launch from parity g.par: up to max_steps supersteps (0: no
+// limit). Returns its control block after the launch completes.
+int run_sparse(uint64_t max_steps, SparseCtl& out)
+{
+  hipLaunchKernelGGL(k_sparse, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
+    (unsigned long long)max_steps, g.d_ctl);
+  HIPCK(hipGetLastError());
+  HIPCK(hipMemcpyAsync(g.h_ctl, g.d_ctl, sizeof(SparseCtl), hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  out = *g.h_ctl;
+  g.par = out.par;
+  g.sparse_launches++;
+  g.sparse_steps += out.steps;
+  return 0;
 }
 
 // The scheduler loop to quiescence (or max_steps); caller holds g.mu.
 int run_locked(uint64_t max_steps, uint64_t* steps_done)
 {
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   uint64_t done = 0;
   if(g.n_zones)
   {
@@ -1041,8 +1125,33 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
     rc = pend_read(kPendPre, 1, pv);
     if(rc) return rc;
     unsigned long long before = pv[0];
+    const bool sp = sparse_ok();
     while(before > 0 && (max_steps == 0 || done < max_steps))
     {
+      if(sp && before <= kSpCap)
+      {
+        // few messages in flight: whole supersteps in one workgroup until the
+        // world is quiet, max_steps, or a step needs the zone path
+        SparseCtl c;
+        rc = run_sparse(max_steps ? max_steps - done : 0, c);
+        if(rc) return rc;
+        done += c.steps;
+        if(c.reason == SP_QUIESCENT) { before = 0; break; }
+        if(c.reason == SP_MAX_STEPS) break;
+        if(c.steps && c.pending == 0xFFFFFFFFFFFFFFFFull)
+        {
+          // the last step overflowed the list: count what is pending
+          HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
+          rc = launch_pending(kPendPre);
+          if(rc) return rc;
+          rc = pend_read(kPendPre, 1, pv);
+          if(rc) return rc;
+          before = pv[0];
+          if(before == 0) break;
+        }
+        if(max_steps && done >= max_steps) break;
+        // SP_DENSE: the next steps go through k_step (at least one chunk)
+      }
       uint32_t k = kChunk;
       if(max_steps) k = (uint32_t)std::min<uint64_t>(k, max_steps - done);
       // pend[j] = pending at the start of step j (k_step), pend[k] = after the chunk
@@ -1096,6 +1205,7 @@ GPU_ACTOR_API int gpu_actor_run_async(uint64_t max_steps, gpu_actor_done_fn done
   const int dev = g.device;
   try
   {
+    std::lock_guard<std::mutex> wl(g.wmu);
     g.worker = std::thread([max_steps, done, ctx, dev]() {
       int rc;
       uint64_t steps = 0;
@@ -1142,6 +1252,10 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   if(g.n_zones == 0 || n == 0) return 0;
   // Every kEventStride-th step carries start/stop events (the dispatch's own
   // timestamps, hipExtLaunchKernel); timing every step costs ~5 us of
@@ -1178,6 +1292,10 @@ GPU_ACTOR_API int gpu_actor_sync(void)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   HIPCK(hipStreamSynchronize(g.stream));
   return check_sticky();
 }
@@ -1187,6 +1305,10 @@ GPU_ACTOR_API int gpu_actor_state_read(uint32_t type_id, uint64_t first, uint64_
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   if(type_id >= GPU_ACTOR_MAX_TYPES || !out) return GPU_ACTOR_EINVAL;
   HostType& t = g.types[type_id];
   if(!t.created || first + n > t.lcount) return GPU_ACTOR_EINVAL;
@@ -1203,6 +1325,10 @@ GPU_ACTOR_API int gpu_actor_state_write(uint32_t type_id, uint64_t first, uint64
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   if(type_id >= GPU_ACTOR_MAX_TYPES || !in) return GPU_ACTOR_EINVAL;
   HostType& t = g.types[type_id];
   if(!t.created || first + n > t.lcount) return GPU_ACTOR_EINVAL;
@@ -1218,6 +1344,10 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
+  {
+    const int frc = flush_sends();
+    if(frc) return frc;
+  }
   if(!out) return GPU_ACTOR_EINVAL;
   unsigned long long st[ST_COUNT];
   HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));

@@ -178,8 +178,10 @@ __device__ __forceinline__ XRec xpack(uint32_t to, uint32_t w, uint32_t from, ui
   return x;
 }
 
-// Per-lane bookkeeping while one actor drains.
-struct ActorCtx {
+// Per-lane bookkeeping while one actor drains: the fields every delivery
+// context shares. A context type (ZoneCtx: k_step's zone outbox; SparseCtx:
+// k_sparse's LDS message list) adds put(to, w, arg), the serial send.
+struct ActorBase {
   uint32_t self;         // global id
   uint32_t li;           // index within its type (local)
   uint32_t src_local;    // slot within the zone
@@ -188,11 +190,6 @@ struct ActorCtx {
   uint32_t applied;      // local reducible applies issued
   int      applied_type;
   int      type;         // the draining actor's type
-  ORec*     out;         // zone outbox (global scratch)
-  uint32_t  ocap;        // its capacity
-  uint32_t  nxt;         // landing parity of this step's sends
-  uint32_t* s_nout;      // LDS outbox counter
-  uint32_t* s_hist;      // LDS histogram by bucket
   unsigned long long* agg;   // this wave's LDS aggregation word
   unsigned long long* fan;   // zone accumulators of fan-in applies (LDS, 2 x kFanLds) or null
   int      fan_t;        // analyzer type those accumulators are for
@@ -201,8 +198,28 @@ struct ActorCtx {
   uint32_t rc_first, rc_count, rc_lfirst, rc_lcount;
   uint64_t* rc_state;
   uint64_t rc_mask;
+
+  __device__ __forceinline__ void reset_common()
+  {
+    seq = 0; sent = 0; applied = 0; applied_type = -1;
+    fan = nullptr; fan_t = -1;
+    rc_first = rc_count = rc_lfirst = rc_lcount = 0;
+    rc_state = nullptr;
+    rc_mask = 0;
+  }
 };
 
+struct ZoneCtx;
+__device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg);
+
+struct ZoneCtx : ActorBase {
+  ORec*     out;         // zone outbox (global scratch)
+  uint32_t  ocap;        // its capacity
+  uint32_t  nxt;         // landing parity of this step's sends
+  uint32_t* s_nout;      // LDS outbox counter
+  uint32_t* s_hist;      // LDS histogram by bucket
+  __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg) { outbox_put(*this, to, w, arg); }
+};
 // ---- delivery --------------------------------------------------------------
 
 // Reducible behaviours: applied as device atomics at the owner.
@@ -234,22 +251,22 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
 // Outbox full (a zone sent more than its mailbox capacity this step): land the
 // record directly with its own atomic on the destination bucket's counter. The
 // receiver sorts by key, so where a record lands does not change delivery order.
-__device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint32_t w, uint64_t arg)
+__device__ __forceinline__ void send_direct(uint32_t nxt, uint32_t self, uint32_t to, uint32_t w, uint64_t arg)
 {
   const uint32_t R = c_eng.nranks;
   const uint32_t nz = c_eng.n_zones;
   const uint32_t b = bucket_of(to);
   if(b < nz)
   {
-    const uint32_t pos = atomicAdd(&c_eng.land_n[a.nxt][b], 1u);
+    const uint32_t pos = atomicAdd(&c_eng.land_n[nxt][b], 1u);
     if(pos < zone_capacity(b))
     {
       uint4 v;
       v.x = w | (rdiv(to) & kZoneMask);
-      v.y = a.self;
+      v.y = self;
       v.z = (uint32_t)arg;
       v.w = (uint32_t)(arg >> 32);
-      *reinterpret_cast<uint4*>(c_eng.land[a.nxt] + c_eng.zoff[b] + pos) = v;
+      *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos) = v;
     }
     else
       atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
@@ -259,7 +276,7 @@ __device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint
     const unsigned long long pos = atomicAdd(&c_eng.xcount[b - nz], 1ull);
     if(pos < c_eng.xcap)
     {
-      c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] = xpack(to, w, a.self, arg);
+      c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] = xpack(to, w, self, arg);
     }
     else
       atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], 1ull);
@@ -267,12 +284,12 @@ __device__ __forceinline__ void send_direct(const ActorCtx& a, uint32_t to, uint
 }
 
 // Park one record in the zone outbox and count it in its destination bucket.
-__device__ __forceinline__ void outbox_put(ActorCtx& a, uint32_t to, uint32_t w, uint64_t arg)
+__device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg)
 {
   const uint32_t idx = atomicAdd(a.s_nout, 1u);
   if(idx >= a.ocap)
   {
-    send_direct(a, to, w, arg);
+    send_direct(a.nxt, a.self, to, w, arg);
     return;
   }
   ORec r;
@@ -282,7 +299,8 @@ __device__ __forceinline__ void outbox_put(ActorCtx& a, uint32_t to, uint32_t w,
 }
 
 // A handler's send: stamped with its canonical (sender, seq) key now.
-__device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t beh, uint64_t arg)
+template <class A>
+__device__ __forceinline__ void send_serial(A& a, uint32_t to, uint32_t beh, uint64_t arg)
 {
   a.sent++;
   if(a.seq >= c_eng.seq_max)
@@ -290,7 +308,7 @@ __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t b
     atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
     return;
   }
-  outbox_put(a, to, (a.seq << 16) | (beh << 12), arg);
+  a.put(to, (a.seq << 16) | (beh << 12), arg);
   a.seq++;
 }
 
@@ -298,7 +316,8 @@ __device__ __forceinline__ void send_serial(ActorCtx& a, uint32_t to, uint32_t b
 // gencall.c:606-612): recorded with its canonical key; the id is assigned
 // when the step ends (engine.hip: spawn_process), the constructor message is
 // delivered in the next step. Counts as a send of the creator.
-__device__ __forceinline__ void spawn_actor(ActorCtx& a, uint32_t type, uint32_t beh, uint64_t arg)
+template <class A>
+__device__ __forceinline__ void spawn_actor(A& a, uint32_t type, uint32_t beh, uint64_t arg)
 {
   a.sent++;
   if(a.seq >= c_eng.seq_max)
@@ -326,12 +345,13 @@ __device__ __forceinline__ bool is_remote(uint32_t to)
 // fan-in Analyzer apply, aggregated per wavefront: lanes hitting the same
 // analyzer fold their count and XOR through LDS and one lane issues the two
 // global atomics (Guideline 12: one atomic per (wave, destination)).
-__device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t arg)
+template <class A>
+__device__ __forceinline__ void send_analyzer(A& a, uint32_t to, uint64_t arg)
 {
   a.sent++;
   const bool remote = is_remote(to);
   if(remote)
-    outbox_put(a, to, (kSeqApply << 16) | (GPU_ACTOR_FANIN_MSG << 12), arg);  // counted by owner
+    a.put(to, (kSeqApply << 16) | (GPU_ACTOR_FANIN_MSG << 12), arg);  // counted by owner
   else
   {
     a.applied++;
@@ -377,12 +397,13 @@ __device__ __forceinline__ void send_analyzer(ActorCtx& a, uint32_t to, uint64_t
   }
 }
 
-__device__ __forceinline__ void send_updater(ActorCtx& a, uint32_t to, uint64_t d)
+template <class A>
+__device__ __forceinline__ void send_updater(A& a, uint32_t to, uint64_t d)
 {
   a.sent++;
   if(is_remote(to))
   {
-    outbox_put(a, to, (kSeqApply << 16) | (GPU_ACTOR_GUPS_UPDATE << 12), d);  // counted by owner
+    a.put(to, (kSeqApply << 16) | (GPU_ACTOR_GUPS_UPDATE << 12), d);  // counted by owner
     return;
   }
   a.applied++;
@@ -418,14 +439,12 @@ template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SRC>      { static constexpr int W
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SINK>     { static constexpr int W = 11; };
 template <> struct HT_Words<GPU_ACTOR_HT_SPREADER>      { static constexpr int W = 5; };
 
-template <int HT>
-__device__ __forceinline__ void handle(const TypeDev& T, ActorCtx& a, uint64_t (&s)[HT_Words<HT>::W],
-  uint32_t beh, uint64_t arg, unsigned long long* s_agg);
+template <int HT> struct HtTag {};
 
 // examples/ring/main.pony:13-24
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_RING>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[4], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_RING>, const TypeDev& T, A& a,
+  uint64_t (&s)[4], uint32_t beh, uint64_t arg)
 {
   if(beh == GPU_ACTOR_RING_SET)
   {
@@ -443,9 +462,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_RING>(const TypeDev& T, Acto
 }
 
 // examples/message-ubench/main.pony:265-286 (+ forward budget)
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_PINGER>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[3], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_PINGER>, const TypeDev& T, A& a,
+  uint64_t (&s)[3], uint32_t beh, uint64_t arg)
 {
   s[2] += 1;
   if(s[2] <= T.params[2])
@@ -455,7 +474,8 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_PINGER>(const TypeDev& T, Ac
   }
 }
 
-__device__ __forceinline__ void det_ping(const TypeDev& T, ActorCtx& a, uint64_t& count,
+template <class A>
+__device__ __forceinline__ void det_ping(const TypeDev& T, A& a, uint64_t& count,
   uint64_t& acc, uint32_t beh, uint64_t arg)
 {
   count += 1;
@@ -468,16 +488,16 @@ __device__ __forceinline__ void det_ping(const TypeDev& T, ActorCtx& a, uint64_t
   }
 }
 
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_PINGER_DET>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[2], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_PINGER_DET>, const TypeDev& T, A& a,
+  uint64_t (&s)[2], uint32_t beh, uint64_t arg)
 {
   det_ping(T, a, s[0], s[1], beh, arg);
 }
 
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_STORM>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[2], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_STORM>, const TypeDev& T, A& a,
+  uint64_t (&s)[2], uint32_t beh, uint64_t arg)
 {
   if(beh == GPU_ACTOR_STORM_TOKEN)
   {
@@ -494,9 +514,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_STORM>(const TypeDev& T, Act
 }
 
 // examples/fan-in/main.pony:241-250
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_FANIN_SENDER>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[4], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FANIN_SENDER>, const TypeDev& T, A& a,
+  uint64_t (&s)[4], uint32_t beh, uint64_t arg)
 {
   const uint64_t k = rand_int_unbiased(s[0], s[1], T.params[0]);
   const uint64_t i = a.self - T.first;
@@ -508,9 +528,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_FANIN_SENDER>(const TypeDev&
 }
 
 // examples/gups_basic/main.pony:110-143, one message per datum
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_GUPS_STREAMER>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[2], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_GUPS_STREAMER>, const TypeDev& T, A& a,
+  uint64_t (&s)[2], uint32_t beh, uint64_t arg)
 {
   const uint64_t chunk = T.params[0], shift = T.params[1], mask = T.params[2];
   const uint32_t ubase = (uint32_t)T.params[3];
@@ -527,9 +547,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_GUPS_STREAMER>(const TypeDev
     s[1] = 1;
 }
 
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_FIFO_SRC>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[3], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SRC>, const TypeDev& T, A& a,
+  uint64_t (&s)[3], uint32_t beh, uint64_t arg)
 {
   const uint64_t i = a.self - T.first;
   for(uint64_t j = 0; j < arg; ++j)
@@ -542,9 +562,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_FIFO_SRC>(const TypeDev& T, 
     send_serial(a, a.self, GPU_ACTOR_FIFO_BURST, arg);
 }
 
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_FIFO_SINK>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[11], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SINK>, const TypeDev& T, A& a,
+  uint64_t (&s)[11], uint32_t beh, uint64_t arg)
 {
   const uint64_t ns = T.params[0] ? T.params[0] : 1;
   const uint32_t slot = (uint32_t)(((arg >> 32) / ns) % 8);
@@ -561,9 +581,9 @@ __device__ __forceinline__ void handle<GPU_ACTOR_HT_FIFO_SINK>(const TypeDev& T,
 }
 
 // examples/spreader/main.pony:9-48
-template <>
-__device__ __forceinline__ void handle<GPU_ACTOR_HT_SPREADER>(const TypeDev& T, ActorCtx& a,
-  uint64_t (&s)[5], uint32_t beh, uint64_t arg, unsigned long long* s_agg)
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_SPREADER>, const TypeDev& T, A& a,
+  uint64_t (&s)[5], uint32_t beh, uint64_t arg)
 {
   if(beh == GPU_ACTOR_SPREADER_SPREAD)
   {

@@ -259,7 +259,7 @@ struct AccS {
 // arrival group in (from, seq) key order — and hand the canonical tail to the
 // next step's carry buffer.
 template <int HT, class Acc>
-__device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a, Acc acc,
+__device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, Acc acc,
   uint32_t n, uint32_t nc, ZRec* cout, uint32_t cout_room)
 {
   // a register copy of the type's fields: read once, not re-read after every
@@ -299,7 +299,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
   while(done < hc)
   {
     const ZRec r = acc.rec(done);
-    handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
+    handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
     ++done;
   }
   if(g > 0)
@@ -318,7 +318,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
 #pragma unroll
         for(int j = 0; j < (int)SM; ++j)
           if((uint32_t)j == bi) k[j] = ~0ull;
-        handle<HT>(T, a, s, (uint32_t)best & 0xFu, barg, nullptr);
+        handle(HtTag<HT>{}, T, a, s, (uint32_t)best & 0xFu, barg);
       }
       done += g;
     }
@@ -336,7 +336,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
           if((r == 0 || kk > last) && kk < best) { best = kk; bi = j; }
         }
         const ZRec rr = acc.rec(nc + bi);
-        handle<HT>(T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg, nullptr);
+        handle(HtTag<HT>{}, T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg);
         last = best;
       }
       done += g;
@@ -348,7 +348,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ActorCtx& a,
       for(uint32_t k = 0; k < q; ++k)
       {
         const ZRec r = acc.rec(nc + k);
-        handle<HT>(T, a, s, (r.w0 >> 12) & 0xFu, r.arg, nullptr);
+        handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
       }
       done += q;
     }
@@ -569,8 +569,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.carry_n[nxt][z] = min(ncout, cap);
 
   // ---- 3. run handlers -------------------------------------------------------------
-  ActorCtx a;
-  a.seq = 0; a.sent = 0; a.applied = 0; a.applied_type = -1;
+  ZoneCtx a;
+  a.reset_common();
   a.out = c_eng.O + c_eng.zoff[z];
   a.s_nout = &s_nout;
   a.ocap = cap;
@@ -578,11 +578,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   a.s_hist = s_hist;
   a.agg = &s_agg[wv];
   // fan-in senders fold their analyzer applies per zone in LDS
-  a.fan = nullptr;
-  a.fan_t = -1;
-  a.rc_first = a.rc_count = a.rc_lfirst = a.rc_lcount = 0;
-  a.rc_state = nullptr;
-  a.rc_mask = 0;
   if constexpr(kFan)
     if(tz >= 0 && c_types[tz].ht == GPU_ACTOR_HT_FANIN_SENDER)
     {

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -94,6 +95,8 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
 
 _lib = None
+# set while a run_async completion callback runs on the library's thread
+_IN_CALLBACK = threading.local()
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -221,6 +224,7 @@ class Engine:
         self.first: dict[int, int] = {}
         self.count: dict[int, int] = {}
         self.reserve: dict[int, int] = {}
+        self._thunks: list = []
         self.alive = True
 
     @staticmethod
@@ -283,10 +287,18 @@ class Engine:
         called on that thread when the run ends (the Pony binding sends a
         completion message to a notify actor from there)."""
         def _cb(_ctx, rc, steps):
-            if done is not None:
-                done(rc, steps)
-        self._done_cb = DONE_FN(_cb)      # kept alive until the next run_async
-        _ck("gpu_actor_run_async", self.lib.gpu_actor_run_async(max_steps, self._done_cb, None))
+            _IN_CALLBACK.active = True
+            try:
+                if done is not None:
+                    done(rc, steps)
+            finally:
+                _IN_CALLBACK.active = False
+        thunk = DONE_FN(_cb)
+        rc = self.lib.gpu_actor_run_async(max_steps, thunk, None)
+        _ck("gpu_actor_run_async", rc)
+        # the progress thread holds this pointer until its run ends: keep every
+        # accepted thunk alive until shutdown() (outside a callback) has joined it
+        self._thunks.append(thunk)
 
     def wait(self) -> int:
         """Join the last asynchronous run; returns its step count."""
@@ -349,6 +361,8 @@ class Engine:
         if self.alive:
             _ck("gpu_actor_shutdown", self.lib.gpu_actor_shutdown())
             self.alive = False
+            if not getattr(_IN_CALLBACK, "active", False):
+                self._thunks.clear()      # the progress thread has been joined
             if self._xp is not None:  # drop the callbacks before they are freed
                 self.lib.gpu_actor_set_transport(ALLTOALLV_FN(), ALLREDUCE_FN(), None)
                 self._xp = None

@@ -27,6 +27,22 @@ def _msgs(to, beh, arg) -> np.ndarray:
     return out
 
 
+def _sendv(eng, m: np.ndarray) -> None:
+    """Each rank runs the same Main and injects its own share: the messages
+    addressed to actors it owns (id % n_ranks == rank); the C-ABI rejects the
+    others (include/gpu_actor.h, gpu_actor_sendv)."""
+    r = getattr(eng, "n_ranks", 1)
+    if r > 1:
+        m = m[(m["to"].astype(np.uint64) % np.uint64(r)) == np.uint64(eng.rank)]
+    eng.sendv(m)
+
+
+def _send(eng, to: int, beh: int, arg: int) -> None:
+    r = getattr(eng, "n_ranks", 1)
+    if r == 1 or to % r == eng.rank:
+        eng.send(to, beh, arg)
+
+
 # ---- examples/ring ---------------------------------------------------------------
 def ring(eng, size: int, count: int, passes: int, type_id: int = 0) -> dict:
     """setup_ring (ring/main.pony:61-72): `count` rings of `size` actors; actor 1
@@ -42,7 +58,7 @@ def ring(eng, size: int, count: int, passes: int, type_id: int = 0) -> dict:
     m[1::2] = _msgs(heads, RING_PASS, passes)
     if passes == 0:
         m = m[0::2]
-    eng.sendv(m)
+    _sendv(eng, m)
     return {"type": type_id, "first": first, "n": size * count,
             "total_msgs": count * (passes + 1) + count}
 
@@ -76,7 +92,7 @@ def ubench(eng, n: int, initial: int = 5, budget: int = 100, seed: int = 5489,
         else:
             payload = np.uint64(42)
         parts.append(_msgs(first + i, PINGER_PING, payload))
-    eng.sendv(np.concatenate(parts) if parts else np.empty(0, dtype=MSG_DTYPE))
+    _sendv(eng, np.concatenate(parts) if parts else np.empty(0, dtype=MSG_DTYPE))
     return {"type": type_id, "first": first, "n": n, "det": det}
 
 
@@ -98,7 +114,7 @@ def fanin(eng, senders: int, analyzers: int, msgs: int, seedmode: int = 0,
     eng.type_param(snd_type, 2, msgs)
     eng.type_param(snd_type, 3, seedmode)
     sfirst = eng.create(snd_type, senders)
-    eng.sendv(_msgs(sfirst + np.arange(senders, dtype=np.uint64), FANIN_SEND_MSGS, 0))
+    _sendv(eng, _msgs(sfirst + np.arange(senders, dtype=np.uint64), FANIN_SEND_MSGS, 0))
     return {"an_type": an_type, "snd_type": snd_type, "afirst": afirst, "sfirst": sfirst,
             "total_msgs": 2 * senders * msgs}
 
@@ -124,7 +140,7 @@ def gups(eng, logtable: int = 20, updaters: int = 8, streamers: int = 4, chunk: 
     eng.type_param(str_type, 3, ufirst)
     eng.type_param(str_type, 5, chunk * iterate)
     sfirst = eng.create(str_type, streamers)
-    eng.sendv(_msgs(sfirst + np.arange(streamers, dtype=np.uint64), GUPS_APPLY, iterate))
+    _sendv(eng, _msgs(sfirst + np.arange(streamers, dtype=np.uint64), GUPS_APPLY, iterate))
     return {"up_type": up_type, "str_type": str_type, "size": size, "updaters": updaters,
             "updates": streamers * chunk * (iterate + 1)}
 
@@ -151,7 +167,7 @@ def storm(eng, n: int, r: int = 4, hops: int = 16, seed: int = 5489, type_id: in
     for k in range(r):
         parts.append(_msgs(first + i, STORM_STORM,
                            (i * np.uint64(r) + np.uint64(k)) << np.uint64(32)))
-    eng.sendv(np.concatenate(parts))
+    _sendv(eng, np.concatenate(parts))
     return {"type": type_id, "first": first, "n": n}
 
 
@@ -164,7 +180,7 @@ def spreader(eng, count: int = 10, type_id: int = 0) -> dict:
     nodes = (1 << count) - 1
     eng.type_reserve(type_id, nodes - 1)
     root = eng.create(type_id, 1)
-    eng.send(root, SPREADER_SPREAD, (0xFFFFFFFF << 32) | count)
+    _send(eng, root, SPREADER_SPREAD, (0xFFFFFFFF << 32) | count)
     return {"type": type_id, "root": root, "nodes": nodes}
 
 
@@ -186,7 +202,7 @@ def fifo(eng, sources: int = 64, sinks: int = 8, bursts: int = 10, m: int = 4,
     eng.type_param(src_type, 1, sinks)
     eng.type_param(src_type, 2, bursts)
     sfirst = eng.create(src_type, sources)
-    eng.sendv(_msgs(sfirst + np.arange(sources, dtype=np.uint64), FIFO_BURST, m))
+    _sendv(eng, _msgs(sfirst + np.arange(sources, dtype=np.uint64), FIFO_BURST, m))
     return {"sink_type": sink_type, "src_type": src_type}
 
 
