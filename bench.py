@@ -1,34 +1,47 @@
-"""bench.py — actor msgs/sec on the gpu_actor engine (BASELINE.json metric).
+"""bench.py — actor msgs/sec on the gpu_actor engine (BASELINE.json metric:
+"actor msgs/sec (node), message-ubench & ring").
 
-Workload (BASELINE.json configs[1]): examples/message-ubench
-scaled to 1,048,576 Pinger actors per GPU, 5 initial pings each, steady state
-(no forward budget: every ping is forwarded to pinger rand.int(N), as the
-reference's ping/send_pings do while `_go` is set). One "step" = one superstep:
-every pinger drains its mailbox and forwards each ping.
+Headline workload (BASELINE.json configs[1]): examples/
+message-ubench scaled to 1,048,576 Pinger actors per GPU, 5 initial pings
+each, steady state (no forward budget: every ping is forwarded to pinger
+rand.int(N), as the reference's ping/send_pings do while `_go` is set). One
+"step" = one superstep: every pinger drains its mailbox and forwards each ping.
 
 Weak scaling: each rank owns 1,048,576 pingers of a global population of
 N x 1,048,576 (hash-partitioned, id % N); pings cross GPUs through the RCCL
 exchange. value = delivered messages over all ranks / max-over-ranks time of
 the K timed steps.
 
-Also reported:
-  roofline     — the drain kernel's algorithmic HBM bytes per launch
-                 (32 B per message: 16-B record written by the sender's zone and
-                 read by the receiver's zone; 2*S + 2*M per active actor: state
-                 read + write, S = 24 B for a pinger, and the mailbox head/tail
-                 M = 8 B — SURVEY §8 d3's formula) / its average duration,
-                 timed by HIP events bound to every 8th k_step dispatch of the
-                 timed region (hipExtLaunchKernel, on the engine's stream);
+Also reported on the same line:
+  roofline     — k_step's algorithmic HBM bytes per launch (SURVEY §8 d3:
+                 2 x 16-B record per message + (2S + 2M) per active actor,
+                 S = 24 B pinger state, M = 8 B mailbox head/tail) / its
+                 average duration = two HIP events on the engine's stream
+                 around the K timed launches, / K (includes the launch
+                 boundaries, so it never exceeds ms_per_step); `traffic` =
+                 HBM bytes per launch from the rocprofv3 --pmc passes of the
+                 SAME libgpuactor.so (profiles/pmc_k_step_<tag>.json carries
+                 the library's sha256; null if none matches);
   cpu_baseline — the reference runtime (oracle/_ref/libponyrt.so, built from
-                 KittyMac/ponyc src/libponyrt) running the same pinger graph via
-                 oracle/_ref/harness_ubench on this host's cores (rank 0, N=1).
+                 KittyMac/ponyc src/libponyrt) running the same pinger graph
+                 (oracle/_ref/harness_ubench) on this host: at every usable
+                 physical core (--ponymaxthreads, SURVEY §8 d4, start.c:237-241)
+                 and at 1 thread, median of 5 runs each, same forward budget
+                 for both (rank 0, N=1);
+  ring         — C1, examples/ring --size 1000 --count 100 --pass 10000 on
+                 the GPU (run to quiescence, median of 3) beside the same
+                 reference harness at the same core counts (BASELINE names
+                 "message-ubench & ring"; N=1 only).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--actors A]
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -39,8 +52,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PINGER_STATE_BYTES = 24        # rng x, y + count
-# PMC summary (scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of the current k_step build
-PMC_TAG = "r01i"
 REC_BYTES = 16
 MAILBOX_BYTES = 8              # mailbox head/tail per active actor (SURVEY §8 d3's M)
 # device atomic peak measured on MI355X by scripts/ubench_mem.hip (random u32
@@ -57,8 +68,10 @@ def parse():
     p.add_argument("--initial", type=int, default=5)
     p.add_argument("--mailbox-cap", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-budget", type=int, default=40,
-                   help="forward budget of the bounded CPU sample")
+    p.add_argument("--no-ring", action="store_true")
+    p.add_argument("--cpu-budget", type=int, default=10,
+                   help="forward budget per pinger of the bounded CPU sample")
+    p.add_argument("--cpu-runs", type=int, default=5)
     return p.parse_args()
 
 
@@ -90,15 +103,6 @@ def allmax(pg, v: float) -> float:
     return float(t.item())
 
 
-def allsum(pg, v: float) -> float:
-    if pg is None:
-        return v
-    import torch
-    t = torch.tensor([v], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
-
-
 def bcast_bytes(pg, rank: int, data: bytes | None) -> bytes:
     if pg is None:
         return data
@@ -107,53 +111,149 @@ def bcast_bytes(pg, rank: int, data: bytes | None) -> bytes:
     return obj[0]
 
 
-def cpu_baseline(args) -> dict | None:
-    """Reference libponyrt on this host, bounded sample of the same workload."""
+# ---- host cores -------------------------------------------------------------------------
+def host_cores() -> dict:
+    """Physical cores of this host, and how many of them this process may use
+    (affinity mask and cgroup CPU quota). The reference caps --ponymaxthreads
+    at the physical core count (start.c:237-241)."""
+    phys, model = set(), None
+    try:
+        pid = core = None
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    core = v
+                elif not k and pid is not None:
+                    phys.add((pid, core))
+                    pid = core = None
+        if pid is not None:
+            phys.add((pid, core))
+    except OSError:
+        pass
+    n_phys = len(phys) or (os.cpu_count() or 1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(n_phys, affinity, quota or affinity)
+    return {"model": model, "physical": n_phys, "affinity": affinity, "cgroup_quota": quota,
+            "usable": usable}
+
+
+def _median_runs(pyoracle, harness: str, args: dict, runs: int, timeout: float) -> dict:
+    rates, secs, msgs = [], [], None
+    for _ in range(runs):
+        info, _ = pyoracle.run_harness(harness, args, None, timeout=timeout)
+        rates.append(info["msgs_per_sec"])
+        secs.append(info["seconds"])
+        msgs = info["msgs"]
+    return {"value": round(statistics.median(rates), 1), "runs": [round(r, 1) for r in rates],
+            "msgs": msgs, "seconds_median": round(statistics.median(secs), 4)}
+
+
+def cpu_reference(args, harness: str, hargs: dict, timeout: float) -> dict | None:
+    """The reference libponyrt (oracle/_ref) on this host: all usable physical
+    cores and 1 thread, median of args.cpu_runs runs each."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import pyoracle
     except Exception:
         return None
-    exe = pyoracle.harness_path("ubench")
-    if not os.path.exists(exe):
+    if not os.path.exists(pyoracle.harness_path(harness)):
         return None
-    threads = max(1, min(16, os.cpu_count() or 1))
-    sample = {"pingers": args.actors, "initial": args.initial, "budget": args.cpu_budget,
-              "threads": threads, "noscale": 1}
+    cores = host_cores()
+    n = cores["usable"]
     try:
-        info, _ = pyoracle.run_harness("ubench", sample, None, timeout=300)
+        allc = _median_runs(pyoracle, harness, dict(hargs, threads=n, noscale=1), args.cpu_runs,
+                            timeout)
+        one = _median_runs(pyoracle, harness, dict(hargs, threads=1, noscale=1), args.cpu_runs,
+                           timeout)
     except Exception as exc:       # report, never fake
-        return {"value": None, "unit": "msgs/s", "cores": threads, "kind": "reference",
+        return {"value": None, "unit": "msgs/s", "cores": n, "kind": "reference",
                 "sample": f"failed: {exc!r}"}
-    # SURVEY §8 d4: also the single-thread rate (smaller budget: ~5 s at 1.9 M msgs/s)
-    one = None
-    try:
-        info1, _ = pyoracle.run_harness("ubench", dict(sample, threads=1, budget=4), None,
-                                        timeout=120)
-        one = round(info1["msgs_per_sec"], 1)
-    except Exception:
-        one = None
-    model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
-                         None)
-    except OSError:
-        pass
-    return {"value": round(info["msgs_per_sec"], 1), "unit": "msgs/s", "cores": threads,
-            "value_1thread": one, "cpu_model": model,
-            "kind": "reference",
-            "sample": (f"harness_ubench on KittyMac/ponyc libponyrt (-O3, pthread scaling), "
+    return {"value": allc["value"], "unit": "msgs/s", "cores": n, "kind": "reference",
+            "value_1thread": one["value"], "runs": allc["runs"], "runs_1thread": one["runs"],
+            "host": cores, "msgs_per_run": allc["msgs"],
+            "seconds_median": allc["seconds_median"],
+            "seconds_median_1thread": one["seconds_median"]}
+
+
+def cpu_baseline(args) -> dict | None:
+    r = cpu_reference(args, "ubench", {"pingers": args.actors, "initial": args.initial,
+                                       "budget": args.cpu_budget}, timeout=300)
+    if r and r.get("value") is not None:
+        r["sample"] = (f"harness_ubench on KittyMac/ponyc libponyrt (-O3, pthread scaling): "
                        f"{args.actors} pingers x {args.initial} initial pings, forward budget "
-                       f"{args.cpu_budget} ({info['msgs']} msgs, {info['seconds']:.2f} s), "
-                       f"--ponymaxthreads={threads} --ponynoblock --ponynoscale; value_1thread: "
-                       f"--ponymaxthreads=1, forward budget 4")}
+                       f"{args.cpu_budget} per pinger ({r['msgs_per_run']} msgs per run), "
+                       f"--ponymaxthreads={r['cores']} (every usable physical core) and =1, "
+                       f"--ponynoblock --ponynoscale; median of {args.cpu_runs} runs each; "
+                       f"time = pony_start region (CLOCK_MONOTONIC)")
+    return r
+
+
+# ---- the roofline's traffic field: PMC summary of this exact library ---------------------
+def lib_sha16(path: str) -> str | None:
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_traffic(sha: str | None) -> tuple[float | None, str | None]:
+    if sha is None:
+        return None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_k_step_*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("lib_sha16") == sha and d.get("hbm_bytes_per_launch"):
+            return d["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
+# ---- C1 ring on the GPU ----------------------------------------------------------------------
+def ring_gpu(reps: int = 3) -> dict:
+    from ponyc_amd import workloads as W
+    from ponyc_amd.engine import Engine
+    out = []
+    for _ in range(reps):
+        e = Engine(device=0)
+        W.ring(e, 1000, 100, 10000)
+        e.sync()
+        t0 = time.perf_counter()
+        steps = e.run()
+        e.sync()
+        secs = time.perf_counter() - t0
+        c = e.counts()
+        e.shutdown()
+        out.append((c["delivered"] / secs, secs, steps, c["delivered"], c["dropped"]))
+    out.sort()
+    v, secs, steps, delivered, dropped = out[len(out) // 2]
+    return {"value": round(v, 1), "unit": "msgs/s", "seconds": round(secs, 5), "steps": steps,
+            "ms_per_step": round(secs / steps * 1e3, 5), "delivered": delivered,
+            "dropped": dropped, "runs": [round(o[0], 1) for o in out]}
 
 
 def main():
     args = parse()
     world, rank, local, pg = dist_setup(args)
-    from ponyc_amd.engine import Engine, MSG_DTYPE
+    from ponyc_amd.engine import Engine, MSG_DTYPE, LIB_PATH
 
     comm = None
     if world > 1:
@@ -209,7 +309,7 @@ def main():
     t1 = time.perf_counter()
     barrier(pg)
     local_secs = t1 - t0
-    drain_ms = eng.last_drain_ms()
+    step_ms = eng.last_drain_ms()      # events around the K launches, / K
     c1 = eng.counts()        # summed over ranks by the engine
     secs = allmax(pg, local_secs)
     delivered = c1["delivered"] - c0["delivered"]
@@ -218,29 +318,38 @@ def main():
     dropped = c1["dropped"]
     eng.shutdown()
 
-    # roofline of the drain kernel on this rank (per launch)
+    # roofline of the step kernel on this rank (per launch)
     msgs_per_step = delivered / args.steps / world
     active_per_step = active / args.steps / world
     # B = sum_msgs 2R + sum_active_actors (2S + 2M)
     alg_bytes = (msgs_per_step * 2 * REC_BYTES
                  + active_per_step * (2 * PINGER_STATE_BYTES + 2 * MAILBOX_BYTES))
-    achieved = alg_bytes / (drain_ms * 1e-3) / 1e9 if drain_ms > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_step_%s.json" % PMC_TAG)
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    achieved = alg_bytes / (step_ms * 1e-3) / 1e9 if step_ms > 0 else 0.0
+    sha = lib_sha16(LIB_PATH)
+    traffic, traffic_src = pmc_traffic(sha)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
+    cpu = ring = None
+    if rank == 0 and world == 1:
+        if not args.no_ring:
+            ring = {"workload": "C1 examples/ring --size 1000 --count 100 --pass 10000 "
+                                "(100,000 actors, 1,000,100 pass + 100 set messages), run to "
+                                "quiescence",
+                    **ring_gpu()}
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args)
+            if ring is not None:
+                rc = cpu_reference(args, "ring", {"size": 1000, "count": 100, "pass": 10000},
+                                   timeout=120)
+                if rc and rc.get("value") is not None:
+                    rc["sample"] = (f"harness_ring on KittyMac/ponyc libponyrt, same config, "
+                                    f"--ponymaxthreads={rc['cores']} and =1, median of "
+                                    f"{args.cpu_runs} runs each")
+                ring["cpu_baseline"] = rc
 
     if rank == 0:
         value = delivered / secs
         line = {
-            "metric": "actor msgs/sec (node), message-ubench",
+            "metric": "actor msgs/sec (node), message-ubench & ring",
             "value": round(value, 1),
             "unit": "msgs/s",
             "n_gpus": world,
@@ -266,8 +375,8 @@ def main():
             # delivered message, and their rate against the measured device peak
             "atomics": {
                 "per_msg": round(atomics / max(delivered, 1), 5),
-                "gops": round(atomics / world / args.steps / (drain_ms * 1e-3) / 1e9, 3)
-                if drain_ms > 0 else None,
+                "gops": round(atomics / world / args.steps / (step_ms * 1e-3) / 1e9, 3)
+                if step_ms > 0 else None,
                 "peak_gops": ATOMIC_PEAK_GOPS,
             },
             "dropped": dropped,
@@ -275,10 +384,14 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_step", "kernel_ms": round(drain_ms, 4),
+                "traffic_source": traffic_src,
+                "kernel": "k_step", "kernel_ms": round(step_ms, 5),
+                "kernel_ms_source": "HIP events around the timed launches on the engine stream, / steps",
                 "alg_bytes_per_launch": round(alg_bytes, 1),
+                "lib_sha16": sha,
             },
             "cpu_baseline": cpu,
+            "ring": ring,
         }
         print(json.dumps(line))
     if pg is not None:

@@ -197,8 +197,9 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out);
 GPU_ACTOR_API uint32_t gpu_actor_owner(uint64_t id);
 /* Device stream the engine runs on (hipStream_t), for profiling/overlap. */
 GPU_ACTOR_API void* gpu_actor_stream(void);
-/* Average duration (ms) of the drain kernel over the last gpu_actor_run_fixed,
- * measured with HIP events on the engine's stream; 0 if unavailable. */
+/* Average step time (ms) of the last gpu_actor_run_fixed: two HIP events on
+ * the engine's stream around its n launches, divided by n (an upper bound on
+ * the step kernel's own duration); 0 if unavailable. */
 GPU_ACTOR_API double gpu_actor_last_drain_ms(void);
 GPU_ACTOR_API const char* gpu_actor_strerror(int code);
 

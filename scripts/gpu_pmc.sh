@@ -7,6 +7,8 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
+# the library these passes profile: bench.py uses the summary only for this build
+sha256sum ponyc_amd/libgpuactor.so | cut -c1-16 > $OUT/lib_sha16.txt
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || exit $?
 have() { grep -qw "$1" $OUT/counters_list.txt; }
 i=0
@@ -18,7 +20,7 @@ while read -r line; do
   i=$((i+1))
   echo "pass $i:$sel"
   timeout -s KILL 90 rocprofv3 --pmc $sel --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
-    python3 bench.py --no-cpu-baseline --steps 6 --warmup 2 > $OUT/bench_p$i.json 2> $OUT/err_p$i.txt || exit $?
+    python3 bench.py --no-cpu-baseline --no-ring --steps 6 --warmup 2 > $OUT/bench_p$i.json 2> $OUT/err_p$i.txt || exit $?
 done <<'PASSES'
 FETCH_SIZE
 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum

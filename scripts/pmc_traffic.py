@@ -40,6 +40,8 @@ out = {
                     if "TCC_HIT_sum" in mean else None),
     "counters_mean_per_dispatch": mean,
     "correction": "read = FETCH_SIZE x 1024 x 2 (gfx950 half-count on wide reads); write = WRITE_SIZE x 1024",
+    "lib_sha16": (open(os.path.join(d, "lib_sha16.txt")).read().strip()
+                  if os.path.exists(os.path.join(d, "lib_sha16.txt")) else None),
 }
 if fetch_kb is not None and write_kb is not None:
     out["hbm_bytes_per_launch"] = out["read_bytes_corrected"] + out["write_bytes"]
