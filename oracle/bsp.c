@@ -12,8 +12,8 @@
  *   - an emitted message is appended to the receiver's mailbox and is first
  *     visible in step s+1; so each step's arrivals are ordered by
  *     (sender id, sender sequence), after carried-over mail;
- *   - a message whose append would take the mailbox past `cap` slots beyond
- *     the head at the start of the step is dropped and counted;
+ *   - mailboxes are unbounded (as the reference's messageq is): nothing is
+ *     ever dropped; `cap` only sizes the engine's first buffers;
  *   - messages to "reducible" types (all behaviours commutative) are applied
  *     when sent;
  *   - host sends are appended in call order (ids above every actor).
@@ -62,7 +62,7 @@ static struct {
 } S;
 
 static const uint32_t DEFAULT_BATCH = 100;   /* PONY_SCHED_BATCH, actor.c:20 */
-static const uint32_t DEFAULT_CAP = 64;
+static const uint32_t DEFAULT_CAP = 16;   /* engine's initial zone sizing; no limit here */
 
 static int ht_reducible(uint32_t ht)
 {
@@ -261,7 +261,6 @@ static void deliver(uint64_t to, uint32_t beh, uint64_t arg)
     return;
   }
   mbox_t* m = &S.mb[to];
-  if(m->tail - m->head_start >= t->cap) { S.dropped++; return; }
   if(m->tail - m->head >= m->cap_alloc)
   {
     uint64_t nc = m->cap_alloc ? m->cap_alloc * 2 : 8;

@@ -162,6 +162,25 @@ __global__ void k_spawn_commit(const uint32_t* tcnt, unsigned long long* live)
   live[t] += tcnt[t] < room ? tcnt[t] : room;
 }
 
+// ---- records past a zone's capacity (SpillRec, engine_dev.h) ----------------
+// need[z] = largest position + 1 spilled into zone z (either buffer)
+__global__ void __launch_bounds__(kBlock) k_spill_need(const SpillRec* s, uint32_t n, uint32_t* need)
+{
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if(i >= n) return;
+  atomicMax(&need[s[i].z], (s[i].tag & kSpillPosMask) + 1u);
+}
+
+// after the zones have grown: every spilled record to its own position
+__global__ void __launch_bounds__(kBlock) k_spill_place(const SpillRec* s, uint32_t n, uint32_t p)
+{
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if(i >= n) return;
+  const SpillRec r = s[i];
+  ZRec* base = (r.tag & kSpillCarry) ? c_eng.carry[p] : c_eng.land[p];
+  base[c_eng.zoff[r.z] + (r.tag & kSpillPosMask)] = r.rec;
+}
+
 // ===========================================================================
 // Host side
 // ===========================================================================
@@ -249,6 +268,21 @@ struct Engine {
   unsigned long long* d_live = nullptr;  // [GPU_ACTOR_MAX_TYPES] live actors per type
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  // records past zone capacity: spill lists, their counters, and the minimum
+  // capacity each zone has grown to
+  struct SpillStat {
+    unsigned int spill_n[2];
+    unsigned int halt;
+    unsigned int pad;
+    unsigned long long skipped;
+  };
+  SpillRec* d_spill[2] = {nullptr, nullptr};
+  uint32_t spill_cap = 0;
+  SpillStat* d_sstat = nullptr;
+  SpillStat* h_sstat = nullptr;           // pinned
+  uint32_t* d_need = nullptr;
+  std::vector<uint32_t> zcap_min, zcap_host;
+  uint64_t fixups = 0;
   // small-step path (k_sparse)
   SparseCtl* d_ctl = nullptr;
   SparseCtl* h_ctl = nullptr;             // pinned
@@ -329,8 +363,108 @@ int upload_types()
   e.dbg = g.d_dbg;
   e.spawn_key = g.d_skey[0]; e.spawn_arg = g.d_sarg[0];
   e.spawn_n = g.d_spawn_n; e.spawn_cap = g.spawn_cap;
+  e.spill[0] = g.d_spill[0]; e.spill[1] = g.d_spill[1];
+  e.spill_n = g.d_sstat ? g.d_sstat->spill_n : nullptr;
+  e.halt = g.d_sstat ? &g.d_sstat->halt : nullptr;
+  e.skipped = g.d_sstat ? &g.d_sstat->skipped : nullptr;
+  e.spill_cap = g.spill_cap;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
+  return 0;
+}
+
+// Spill lists of at least `cap` records per parity (they start empty between
+// steps, so growing them moves nothing).
+int ensure_spill(uint64_t cap)
+{
+  cap = std::min<uint64_t>(cap, 0x7FFFFFFFull);
+  if(cap <= g.spill_cap) return 0;
+  for(int p = 0; p < 2; ++p)
+  {
+    if(g.d_spill[p]) HIPCK(hipFree(g.d_spill[p]));
+    g.d_spill[p] = nullptr;
+    HIPCK(hipMalloc(&g.d_spill[p], cap * sizeof(SpillRec)));
+  }
+  g.spill_cap = (uint32_t)cap;
+  return 0;
+}
+
+int relayout_zones();
+int upload_types();
+
+int read_sstat()
+{
+  HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+    g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  return 0;
+}
+
+inline bool spill_pending()
+{
+  return g.h_sstat->spill_n[0] || g.h_sstat->spill_n[1] || g.h_sstat->halt;
+}
+
+// Grow every zone that spilled, land the spilled records at the positions
+// they were given, and release the halt (SpillRec, engine_dev.h). Uses the
+// status last read into h_sstat. Nothing is dropped unless a spill list
+// itself overflowed (counted; the run then fails with GPU_ACTOR_EMAILBOX).
+int fixup_spill()
+{
+  const Engine::SpillStat st = *g.h_sstat;
+  if(!st.spill_n[0] && !st.spill_n[1] && !st.halt) return 0;
+  uint32_t n[2], most = 0;
+  for(int p = 0; p < 2; ++p)
+  {
+    n[p] = std::min(st.spill_n[p], g.spill_cap);
+    most = std::max(most, st.spill_n[p]);
+  }
+  if(n[0] || n[1])
+  {
+    const uint32_t nz = g.n_zones;
+    HIPCK(hipMemsetAsync(g.d_need, 0, nz * sizeof(uint32_t), g.stream));
+    for(int p = 0; p < 2; ++p)
+      if(n[p])
+        hipLaunchKernelGGL(k_spill_need, dim3(blocks_for(n[p])), dim3(kBlock), 0, g.stream,
+          (const SpillRec*)g.d_spill[p], n[p], g.d_need);
+    HIPCK(hipGetLastError());
+    std::vector<uint32_t> need(nz);
+    HIPCK(hipMemcpyAsync(need.data(), g.d_need, nz * sizeof(uint32_t), hipMemcpyDeviceToHost,
+      g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    bool grow = false;
+    for(uint32_t z = 0; z < nz; ++z)
+      if(need[z] > g.zcap_host[z])
+      {
+        // double, or 1.5x what this step needed: a burst seldom grows a zone twice
+        const uint64_t want = std::max<uint64_t>(2ull * g.zcap_host[z], need[z] + need[z] / 2);
+        g.zcap_min[z] = (uint32_t)std::min<uint64_t>((want + 15) & ~15ull, kSpillPosMask);
+        grow = true;
+      }
+    if(grow)
+    {
+      int rc = relayout_zones();
+      if(rc) return rc;
+      rc = upload_types();
+      if(rc) return rc;
+    }
+    for(int p = 0; p < 2; ++p)
+      if(n[p])
+        hipLaunchKernelGGL(k_spill_place, dim3(blocks_for(n[p])), dim3(kBlock), 0, g.stream,
+          (const SpillRec*)g.d_spill[p], n[p], (uint32_t)p);
+    HIPCK(hipGetLastError());
+  }
+  HIPCK(hipMemsetAsync(g.d_sstat, 0, sizeof(Engine::SpillStat), g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
+  g.fixups++;
+  // a list that overflowed lost records (counted as dropped): make it larger
+  if(most > g.spill_cap)
+  {
+    const int rc = ensure_spill(2ull * most);
+    if(rc) return rc;
+    return upload_types();
+  }
   return 0;
 }
 
@@ -356,9 +490,11 @@ int relayout_zones()
   std::vector<uint32_t> cap(nz);
   std::vector<uint64_t> off(nz);
   uint64_t total = 0;
+  if(g.zcap_min.size() < nz) g.zcap_min.resize(nz, 0);
   for(uint32_t z = 0; z < nz; ++z)
   {
-    if(cap64[z] > 0xFFFFFFF0ull) return GPU_ACTOR_ERANGE;
+    cap64[z] = std::max<uint64_t>(cap64[z], g.zcap_min[z]);
+    if(cap64[z] > (uint64_t)kSpillPosMask) return GPU_ACTOR_ERANGE;
     cap[z] = (uint32_t)cap64[z];
     off[z] = total;
     total += (cap[z] + 15u) & ~15u;          // keep every zone 256-B aligned
@@ -409,7 +545,8 @@ int relayout_zones()
   g.d_zcap = d_cap;
   g.zone_records = total;
   g.n_zones = nz;
-  return 0;
+  g.zcap_host = cap;
+  return ensure_spill(std::max<uint64_t>(1u << 20, total / 4));
 }
 
 uint32_t required_words(uint32_t ht)
@@ -611,6 +748,15 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   {
     int rc = exchange(g.par);
     if(rc) return rc;
+    // steps never halt on the device with n_ranks > 1 (ranks would part
+    // ways): a zone that overflowed is grown before the next step
+    rc = read_sstat();
+    if(rc) return rc;
+    if(spill_pending())
+    {
+      rc = fixup_spill();
+      if(rc) return rc;
+    }
   }
   if(g.spawn_cap)
   {
@@ -681,6 +827,11 @@ void free_all()
   if(g.d_tcnt) (void)hipFree(g.d_tcnt);
   if(g.d_live) (void)hipFree(g.d_live);
   if(g.d_ctl) (void)hipFree(g.d_ctl);
+  for(int p = 0; p < 2; ++p)
+    if(g.d_spill[p]) (void)hipFree(g.d_spill[p]);
+  if(g.d_sstat) (void)hipFree(g.d_sstat);
+  if(g.h_sstat) (void)hipHostFree(g.h_sstat);
+  if(g.d_need) (void)hipFree(g.d_need);
   if(g.h_ctl) (void)hipHostFree(g.h_ctl);
   if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
@@ -724,8 +875,10 @@ int inject_locked(const gpu_msg_t* first, uint64_t n)
     HIPCK(hipGetLastError());
   }
   g.host_seq += n;
-  HIPCK(hipStreamSynchronize(g.stream));    // the caller may reuse its buffer
-  return 0;
+  // the caller may reuse its buffer: this synchronises the stream
+  int rc = read_sstat();
+  if(rc) return rc;
+  return spill_pending() ? fixup_spill() : 0;
 }
 
 // gpu_actor_send's deferred messages, injected in call order.
@@ -815,6 +968,11 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_tcnt, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
   HIPCK(hipMalloc(&g.d_live, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long)));
   HIPCK(hipMalloc(&g.d_ctl, sizeof(SparseCtl)));
+  HIPCK(hipMalloc(&g.d_sstat, sizeof(Engine::SpillStat)));
+  HIPCK(hipMemsetAsync(g.d_sstat, 0, sizeof(Engine::SpillStat), g.stream));
+  HIPCK(hipHostMalloc(&g.h_sstat, sizeof(Engine::SpillStat), hipHostMallocDefault));
+  memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
+  HIPCK(hipMalloc(&g.d_need, kMaxZones * sizeof(uint32_t)));
   HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
   HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
@@ -890,6 +1048,8 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
+  g.d_spill[0] = g.d_spill[1] = nullptr; g.spill_cap = 0; g.d_sstat = nullptr; g.h_sstat = nullptr;
+  g.d_need = nullptr; g.zcap_min.clear(); g.zcap_host.clear(); g.fixups = 0;
   g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;
   for(int p = 0; p < 2; ++p) g.d_skey[p] = g.d_sarg[p] = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
@@ -1097,6 +1257,8 @@ int run_sparse(uint64_t max_steps, SparseCtl& out)
     (unsigned long long)max_steps, g.d_ctl);
   HIPCK(hipGetLastError());
   HIPCK(hipMemcpyAsync(g.h_ctl, g.d_ctl, sizeof(SparseCtl), hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+    g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   out = *g.h_ctl;
   g.par = out.par;
@@ -1105,7 +1267,24 @@ int run_sparse(uint64_t max_steps, SparseCtl& out)
   return 0;
 }
 
+// Pending mail now (all ranks).
+int pending_now(unsigned long long& out)
+{
+  HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
+  int rc = launch_pending(kPendPre);
+  if(rc) return rc;
+  std::vector<unsigned long long> pv;
+  rc = pend_read(kPendPre, 1, pv);
+  if(rc) return rc;
+  out = pv[0];
+  return 0;
+}
+
 // The scheduler loop to quiescence (or max_steps); caller holds g.mu.
+// One rank: chunks of kChunk k_step launches with one readback each, or
+// k_sparse launches while few records are pending. A zone that overflowed
+// halts the steps after it on the device; the host then grows the zones
+// (fixup_spill) and resumes from the first step that did not run.
 int run_locked(uint64_t max_steps, uint64_t* steps_done)
 {
   if(!g.init) return GPU_ACTOR_ESTATE;
@@ -1116,13 +1295,15 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
   uint64_t done = 0;
   if(g.n_zones)
   {
-    HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-    int rc = launch_pending(kPendPre);
+    int rc = read_sstat();
+    if(rc) return rc;
+    rc = fixup_spill();
+    if(rc) return rc;
+    unsigned long long before = 0;
+    rc = pending_now(before);
     if(rc) return rc;
     std::vector<unsigned long long> pv;
-    rc = pend_read(kPendPre, 1, pv);
-    if(rc) return rc;
-    unsigned long long before = pv[0];
+    std::vector<uint32_t> par_at(kChunk + 1);
     const bool sp = sparse_ok();
     while(before > 0 && (max_steps == 0 || done < max_steps))
     {
@@ -1134,17 +1315,21 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
         rc = run_sparse(max_steps ? max_steps - done : 0, c);
         if(rc) return rc;
         done += c.steps;
+        if(spill_pending())
+        {
+          rc = fixup_spill();
+          if(rc) return rc;
+          rc = pending_now(before);
+          if(rc) return rc;
+          continue;
+        }
         if(c.reason == SP_QUIESCENT) { before = 0; break; }
         if(c.reason == SP_MAX_STEPS) break;
         if(c.steps && c.pending == 0xFFFFFFFFFFFFFFFFull)
         {
           // the last step overflowed the list: count what is pending
-          HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
-          rc = launch_pending(kPendPre);
+          rc = pending_now(before);
           if(rc) return rc;
-          rc = pend_read(kPendPre, 1, pv);
-          if(rc) return rc;
-          before = pv[0];
           if(before == 0) break;
         }
         if(max_steps && done >= max_steps) break;
@@ -1156,17 +1341,33 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       HIPCK(hipMemsetAsync(g.d_pend, 0, (k + 1) * sizeof(unsigned long long), g.stream));
       for(uint32_t j = 0; j < k; ++j)
       {
+        par_at[j] = g.par;
         rc = launch_step(j, nullptr, nullptr);
         if(rc) return rc;
       }
+      par_at[k] = g.par;
       rc = launch_pending(k);
       if(rc) return rc;
+      HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+        g.stream));
       rc = pend_read(0, k + 1, pv);
       if(rc) return rc;
-      for(uint32_t j = 0; j < k && before > 0; ++j)
+      uint32_t j = 0;
+      bool halted = false;
+      for(; j < k && before > 0; ++j)
       {
+        if(pv[j] == kPendSkipped) { halted = true; break; }
         ++done;
         before = pv[j + 1];
+      }
+      if(halted || spill_pending())
+      {
+        // steps from j on did not run: resume at the parity step j would have read
+        if(halted) g.par = par_at[j];
+        rc = fixup_spill();
+        if(rc) return rc;
+        rc = pending_now(before);
+        if(rc) return rc;
       }
     }
   }
@@ -1262,18 +1463,38 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   // wall step).
   int rc = ensure_events(2);
   if(rc) return rc;
-  HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-  HIPCK(hipEventRecord(g.ev[0], g.stream));
-  for(uint64_t j = 0; j < n; ++j)
+  rc = read_sstat();
+  if(rc) return rc;
+  rc = fixup_spill();
+  if(rc) return rc;
+  uint64_t left = n;
+  double ms_total = 0.0;
+  while(left)
   {
-    rc = launch_step((uint32_t)(j % kPendPre), nullptr, nullptr);
+    HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
+    const uint32_t par0 = g.par;
+    HIPCK(hipEventRecord(g.ev[0], g.stream));
+    for(uint64_t j = 0; j < left; ++j)
+    {
+      rc = launch_step((uint32_t)(j % kPendPre), nullptr, nullptr);
+      if(rc) return rc;
+    }
+    HIPCK(hipEventRecord(g.ev[1], g.stream));
+    rc = read_sstat();                      // synchronises the stream
     if(rc) return rc;
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, g.ev[0], g.ev[1]));
+    ms_total += ms;
+    if(!spill_pending()) break;
+    // steps after an overflow did not run (one rank): grow, then run them
+    const uint64_t skipped = std::min<uint64_t>(g.h_sstat->skipped, left);
+    const uint64_t ran = left - skipped;
+    if(R() == 1 && skipped) g.par = par0 ^ (uint32_t)(ran & 1u);
+    rc = fixup_spill();
+    if(rc) return rc;
+    left = skipped;
   }
-  HIPCK(hipEventRecord(g.ev[1], g.stream));
-  HIPCK(hipStreamSynchronize(g.stream));
-  float ms = 0.f;
-  HIPCK(hipEventElapsedTime(&ms, g.ev[0], g.ev[1]));
-  g.last_drain_ms = (double)ms / (double)n;
+  g.last_drain_ms = ms_total / (double)n;
   g.steps_total += n;
   g.host_seq = 0;
   return check_sticky();
@@ -1403,6 +1624,19 @@ GPU_ACTOR_API uint32_t gpu_actor_owner(uint64_t id)
 GPU_ACTOR_API void* gpu_actor_stream(void) { return (void*)g.stream; }
 
 GPU_ACTOR_API double gpu_actor_last_drain_ms(void) { return g.last_drain_ms; }
+
+// Diagnostic (not in the public header): engine internals for tests.
+// out[0] spill fixups, [1] k_sparse launches, [2] supersteps run by k_sparse,
+// [3] zone buffer records, [4] spill list capacity, [5] zones.
+GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init || !out) return GPU_ACTOR_ESTATE;
+  const uint64_t v[6] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+                         g.n_zones};
+  for(uint64_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
+  return 0;
+}
 
 // Diagnostic (not in the public header): phase stamps of the last k_step of
 // a -DGPA_STAMPS build, [n_zones][8] shader-clock values.

@@ -74,6 +74,21 @@ struct XRec {
   uint32_t w1;
   uint64_t arg;
 };
+// A record that found its zone buffer full: kept with the position it was
+// given (landing: its reserved slot; carry: its canonical carry position), so
+// once the host has grown the zone it lands exactly where it would have.
+// tag = pos | kind << 30 (kSpillCarry) ; one list per parity of the buffer.
+struct SpillRec {        // 32 B (16-B aligned halves)
+  ZRec     rec;
+  uint32_t z;
+  uint32_t tag;
+  uint32_t pad[2];
+};
+static_assert(sizeof(SpillRec) == 32, "SpillRec is 32 B");
+constexpr uint32_t kSpillCarry = 1u << 30;
+constexpr uint32_t kSpillPosMask = kSpillCarry - 1;
+constexpr unsigned long long kPendSkipped = ~0ull;   // pend[] mark of a step that did not run
+
 constexpr uint32_t kXSeqApply = 0x3FFFu;
 constexpr uint32_t kXSeqMax = 0x3FFEu;
 static_assert(sizeof(XRec) == 16, "XRec is 16 B");
@@ -117,6 +132,14 @@ struct EngDev {
   uint64_t* spawn_arg;
   unsigned int* spawn_n;          // records written (may exceed spawn_cap: overflow)
   uint32_t spawn_cap, pad3;
+  // zone buffers past capacity (never dropped): spill[p] holds the records
+  // for parity p's landing/carry buffers; a step that finds spill_n[cur] or
+  // halt set does not run (one rank) until the host has grown the zones
+  SpillRec* spill[2];
+  unsigned int* spill_n;          // [2]
+  unsigned int* halt;             // set by a skipped step: every later step skips too
+  unsigned long long* skipped;    // steps skipped since the last fixup
+  uint32_t spill_cap, pad4;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -248,6 +271,30 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
   (void)beh;
 }
 
+// A record whose zone buffer (parity p, landing or carry) is full at `pos`.
+__device__ __forceinline__ void spill_rec(uint32_t p, uint32_t kind, uint32_t z, uint32_t pos,
+  const uint4& v)
+{
+  const unsigned int i = atomicAdd(&c_eng.spill_n[p], 1u);
+  if(i < c_eng.spill_cap)
+  {
+    uint32_t* d = reinterpret_cast<uint32_t*>(c_eng.spill[p] + i);
+    *reinterpret_cast<uint4*>(d) = v;
+    *reinterpret_cast<uint4*>(d + 4) = make_uint4(z, pos | kind, 0u, 0u);
+  }
+  else
+    atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);   // the spill list itself is full
+}
+
+// Store landing record v of zone z at reserved position pos of parity p.
+__device__ __forceinline__ void land_store(uint32_t p, uint32_t z, uint32_t pos, const uint4& v)
+{
+  if(pos < zone_capacity(z))
+    *reinterpret_cast<uint4*>(c_eng.land[p] + c_eng.zoff[z] + pos) = v;
+  else
+    spill_rec(p, 0u, z, pos, v);
+}
+
 // Outbox full (a zone sent more than its mailbox capacity this step): land the
 // record directly with its own atomic on the destination bucket's counter. The
 // receiver sorts by key, so where a record lands does not change delivery order.
@@ -259,17 +306,12 @@ __device__ __forceinline__ void send_direct(uint32_t nxt, uint32_t self, uint32_
   if(b < nz)
   {
     const uint32_t pos = atomicAdd(&c_eng.land_n[nxt][b], 1u);
-    if(pos < zone_capacity(b))
-    {
-      uint4 v;
-      v.x = w | (rdiv(to) & kZoneMask);
-      v.y = self;
-      v.z = (uint32_t)arg;
-      v.w = (uint32_t)(arg >> 32);
-      *reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos) = v;
-    }
-    else
-      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    uint4 v;
+    v.x = w | (rdiv(to) & kZoneMask);
+    v.y = self;
+    v.z = (uint32_t)arg;
+    v.w = (uint32_t)(arg >> 32);
+    land_store(nxt, b, pos, v);
   }
   else
   {

@@ -98,17 +98,12 @@ __device__ void sp_land(const SpList& l, uint32_t n, uint32_t p)
     const uint32_t L = (uint32_t)(l.K[i] >> 32);
     const uint32_t z = L >> kZoneBits;
     const uint32_t pos = atomicAdd(&c_eng.land_n[p][z], 1u);
-    if(pos < zone_capacity(z))
-    {
-      uint4 v;
-      v.x = l.W[i] | (L & kZoneMask);
-      v.y = (uint32_t)l.K[i];
-      v.z = (uint32_t)l.A[i];
-      v.w = (uint32_t)(l.A[i] >> 32);
-      *reinterpret_cast<uint4*>(c_eng.land[p] + c_eng.zoff[z] + pos) = v;
-    }
-    else
-      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+    uint4 v;
+    v.x = l.W[i] | (L & kZoneMask);
+    v.y = (uint32_t)l.K[i];
+    v.z = (uint32_t)l.A[i];
+    v.w = (uint32_t)(l.A[i] >> 32);
+    land_store(p, z, pos, v);
   }
 }
 
@@ -220,7 +215,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
   uint32_t run = sp_block_excl_scan(mine, s_tmp, total);
   for(uint32_t z = z0; z < z1; ++z) { const uint32_t c = s_zpre[z]; s_zpre[z] = run; run += c; }
   if(tid == 0) s_zpre[nz] = total;
-  if(__syncthreads_or(carried) || total > kSpCap)
+  const bool pending_fixup = c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u;
+  if(__syncthreads_or(carried) || total > kSpCap || pending_fixup)
   {
     // the dense path owns this step: nothing was touched
     if(tid == 0)

@@ -260,7 +260,7 @@ struct AccS {
 // next step's carry buffer.
 template <int HT, class Acc>
 __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, Acc acc,
-  uint32_t n, uint32_t nc, ZRec* cout, uint32_t cout_room)
+  uint32_t n, uint32_t nc, uint32_t z, uint32_t co)
 {
   // a register copy of the type's fields: read once, not re-read after every
   // store the handlers make (the compiler cannot prove they do not alias)
@@ -355,18 +355,20 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   }
 #pragma unroll
   for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
-  // the unhandled tail, canonical, becomes next step's carried mail
+  // the unhandled tail, canonical, becomes next step's carried mail (its
+  // positions run past the zone's capacity into the spill list, never lost)
+  ZRec* cout = c_eng.carry[a.nxt] + c_eng.zoff[z];
+  const uint32_t cap = zone_capacity(z);
   for(uint32_t k = done; k < n; ++k)
   {
-    if(k - done < cout_room)
-    {
-      const ZRec r = acc.rec(k);
-      uint4 u;
-      u.x = r.w0; u.y = r.from; u.z = (uint32_t)r.arg; u.w = (uint32_t)(r.arg >> 32);
-      *reinterpret_cast<uint4*>(cout + (k - done)) = u;
-    }
+    const ZRec r = acc.rec(k);
+    uint4 u;
+    u.x = r.w0; u.y = r.from; u.z = (uint32_t)r.arg; u.w = (uint32_t)(r.arg >> 32);
+    const uint32_t pos = co + (k - done);
+    if(pos < cap)
+      *reinterpret_cast<uint4*>(cout + pos) = u;
     else
-      atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+      spill_rec(a.nxt, kSpillCarry, z, pos, u);
   }
   return done;
 }
@@ -398,6 +400,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
   const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // One rank: a zone buffer overflowed into the spill list. The host grows the
+  // zones and lands those records before another step runs; until then every
+  // step is a no-op (spill_n[cur] is final for this launch; halt is set only
+  // by skipped steps, so every zone of a launch decides alike).
+  if(c_eng.nranks == 1 && (c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u))
+  {
+    if(z == 0 && tid == 0)
+    {
+      *c_eng.halt = 1u;
+      c_eng.pend[pend_slot] = kPendSkipped;
+      atomicAdd(c_eng.skipped, 1ull);
+    }
+    return;
+  }
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
   if constexpr(kFan)
     for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
@@ -566,7 +582,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // already its own exclusive scan
   const uint32_t ncout = __syncthreads_or(any_rem) ? block_scan_zone(s_aux, s_tmp) : 0u;
   if(tid == 0)
-    c_eng.carry_n[nxt][z] = min(ncout, cap);
+    c_eng.carry_n[nxt][z] = ncout;          // past cap: the tail is in the spill list
 
   // ---- 3. run handlers -------------------------------------------------------------
   ZoneCtx a;
@@ -584,7 +600,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       a.fan_t = type_of_global((uint32_t)c_types[tz].params[1]);
       if(a.fan_t >= 0) a.fan = s_fan;
     }
-  ZRec* Cout = c_eng.carry[nxt] + c_eng.zoff[z];
   uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
   // drain local actor i, of type t (T = c_types[t])
   auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
@@ -596,16 +611,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     a.type = t;
     a.seq = 0;
     const uint32_t co = s_aux[i];
-    const uint32_t room = co < cap ? cap - co : 0u;
     uint32_t d = 0;
 #define ZDRAIN(HT)                                                                    \
     if(use_idx)                                                                       \
     {                                                                                 \
       AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                        \
-      d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], Cout + co, room);                   \
+      d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], z, co);                              \
     }                                                                                 \
     else                                                                              \
-      d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], Cout + co, room);
+      d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], z, co);
     if constexpr(HTS >= 0)
     {
       ZDRAIN(HTS)
@@ -705,17 +719,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     const uint32_t from = (L0 + (r.y & kZoneMask)) * R + me;
     if(b < nz)
     {
+      uint4 v;
+      v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
+      v.y = from;
+      v.z = r.z;
+      v.w = r.w;
       if(pos < zone_capacity(b))
-      {
-        uint4 v;
-        v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
-        v.y = from;
-        v.z = r.z;
-        v.w = r.w;
         st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
-      }
       else
-        ++dropped;
+        spill_rec(nxt, 0u, b, pos, v);
     }
     else
     {
@@ -866,17 +878,12 @@ __device__ __forceinline__ void land_records(LandRec (&r)[kLandPer], uint32_t cu
     if(r[u].valid)
     {
       const uint32_t pos = s_base[zt[u]] + rk[u];
-      if(pos < zone_capacity(zt[u]))
-      {
-        uint4 v;
-        v.x = r[u].w | (rdiv(r[u].to) & kZoneMask);
-        v.y = r[u].from;
-        v.z = (uint32_t)r[u].arg;
-        v.w = (uint32_t)(r[u].arg >> 32);
-        *reinterpret_cast<uint4*>(c_eng.land[cur] + c_eng.zoff[zt[u]] + pos) = v;
-      }
-      else
-        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+      uint4 v;
+      v.x = r[u].w | (rdiv(r[u].to) & kZoneMask);
+      v.y = r[u].from;
+      v.z = (uint32_t)r[u].arg;
+      v.w = (uint32_t)(r[u].arg >> 32);
+      land_store(cur, zt[u], pos, v);
     }
 }
 

@@ -14,6 +14,7 @@ def _both(engine_factory, oracle, setup, result, run_steps=0, **eng_kw):
     we = setup(e)
     se = e.run(run_steps)
     ce = e.counts()
+    ce["debug"] = e.debug_info()
     re = result(e, we)
     wo = setup(oracle)
     so = oracle.run(run_steps)
@@ -127,18 +128,26 @@ def test_host_sends_between_runs(engine_factory, oracle):
     np.testing.assert_array_equal(ge, go_)
 
 
-def test_mailbox_overflow_reported(engine_factory):
-    e = engine_factory(mailbox_cap=4)
-    W.fanin(e, 10, 1, 3)   # analyzers are reducible; senders need 1 slot
-    e.run()
-    e2 = None
-    from ponyc_amd.engine import GpuActorError
-    e.shutdown()
-    e2 = engine_factory(mailbox_cap=2)
-    W.ubench(e2, 16, initial=5, budget=0)     # 5 initial pings into 2-slot rings
-    with pytest.raises(GpuActorError) as ei:
-        e2.run()
-    assert ei.value.code == -4
+def test_mailbox_overflow_never_drops(engine_factory, oracle):
+    """Zone buffers sized for 2 messages per actor receive 5 at once (host
+    sends) and more per step: the overflow goes to the spill list, the zones
+    grow, and the run equals the unbounded-mailbox oracle (the reference's
+    messageq is unbounded too: messageq.c:31-59)."""
+    g, o = _both(engine_factory, oracle, lambda e: W.ubench(e, 16, initial=5, budget=40),
+                 W.ubench_result, mailbox_cap=2)
+    _assert_same(g, o)
+    assert g[1]["debug"]["fixups"] > 0          # the zones did overflow and grow
+
+
+@pytest.mark.parametrize("batch", [4, 100])
+def test_overflow_in_landing_and_carry(engine_factory, oracle, batch):
+    """Bursts far above the zone capacity during the run (landing) and a
+    backlog past it (carry, batch 4): bit-exact against the oracle, no drops."""
+    g, o = _both(engine_factory, oracle,
+                 lambda e: W.fifo(e, 300, 3, 4, 9, batch=batch, mailbox_cap=1), W.fifo_result,
+                 mailbox_cap=1)
+    _assert_same(g, o)
+    assert g[1]["debug"]["fixups"] > 0
 
 
 # ---- actors created by behaviours (examples/spreader; SURVEY §8 f2) -------------------
