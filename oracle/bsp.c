@@ -33,8 +33,17 @@ typedef struct {
   uint64_t cap_alloc;
   uint64_t head;          /* index of next message to handle (absolute)     */
   uint64_t tail;          /* number of messages ever appended (absolute)     */
-  uint64_t head_start;    /* head at the start of the current step / window  */
+  uint64_t tail0;         /* tail when step `stamp` started (appends in it wait) */
+  uint64_t stamp;         /* step of the first append this step, + 1         */
 } mbox_t;
+
+/* Backpressure state of one actor (actor.c:340-381, 898-921, scheduler.c:
+ * 1496-1635, restated for supersteps — see or_run): overloaded after the
+ * last step it ran, muted, and the receiver it is muted on. */
+typedef struct {
+  uint8_t  o, m;
+  uint32_t r;
+} oflag_t;
 
 typedef struct {
   int      registered, created;
@@ -59,6 +68,18 @@ static struct {
   uint64_t  steps, delivered, sent, dropped;
   ospawn_t* spawns;       /* this step's, in (creator id, call order) order */
   uint64_t  n_spawns, spawns_alloc;
+  /* backpressure: flags, the previous step's end state per actor (bit 0
+   * overloaded, bit 1 muted: either triggers muting), and the actors a step
+   * must visit (mail, muted or overloaded), as a bitmap scanned in id order */
+  oflag_t*  fl;
+  uint8_t*  trig;
+  uint64_t  n_trig;
+  uint64_t* live;
+  uint64_t  pending;
+  /* the actor running now, for send() */
+  uint64_t  cur;
+  int       cur_prev_o, mute_hit, yield_req, running;
+  uint64_t  mute_to;
 } S;
 
 static const uint32_t DEFAULT_BATCH = 100;   /* PONY_SCHED_BATCH, actor.c:20 */
@@ -87,6 +108,9 @@ void or_shutdown(void)
   free(S.mb);
   free(S.type_of);
   free(S.spawns);
+  free(S.fl);
+  free(S.trig);
+  free(S.live);
   memset(&S, 0, sizeof(S));
 }
 
@@ -208,12 +232,19 @@ int or_create(uint32_t type_id, uint64_t count, uint64_t* first_id)
   uint64_t total = S.n_actors + count;
   uint8_t* to = realloc(S.type_of, total ? total : 1);
   mbox_t* mb = realloc(S.mb, (total ? total : 1) * sizeof(mbox_t));
-  if(!to || !mb) return GPU_ACTOR_ENOMEM;
-  S.type_of = to; S.mb = mb;
+  oflag_t* fl = realloc(S.fl, (total ? total : 1) * sizeof(oflag_t));
+  uint8_t* tr = realloc(S.trig, total ? total : 1);
+  const uint64_t words = (total + 63) / 64, old_words = (S.n_actors + 63) / 64;
+  uint64_t* lv = realloc(S.live, (words ? words : 1) * sizeof(uint64_t));
+  if(!to || !mb || !fl || !tr || !lv) return GPU_ACTOR_ENOMEM;
+  S.type_of = to; S.mb = mb; S.fl = fl; S.trig = tr; S.live = lv;
+  for(uint64_t w = old_words; w < words; w++) S.live[w] = 0;
   for(uint64_t a = S.n_actors; a < total; a++)
   {
     S.type_of[a] = (uint8_t)type_id;
     memset(&S.mb[a], 0, sizeof(mbox_t));
+    memset(&S.fl[a], 0, sizeof(oflag_t));
+    S.trig[a] = 0;
   }
   t->first = S.n_actors;
   t->count = count;
@@ -271,14 +302,32 @@ static void deliver(uint64_t to, uint32_t beh, uint64_t arg)
     m->buf = nb;
     m->cap_alloc = nc;
   }
+  /* appended during a step: handled from the next one (BSP visibility) */
+  if(S.running && m->stamp != S.steps + 1)
+  {
+    m->tail0 = m->tail;
+    m->stamp = S.steps + 1;
+  }
   m->buf[m->tail % m->cap_alloc].beh = beh;
   m->buf[m->tail % m->cap_alloc].arg = arg;
   m->tail++;
+  S.pending++;
+  S.live[to >> 6] |= 1ull << (to & 63);
 }
 
 static void send(uint64_t to, uint32_t beh, uint64_t arg)
 {
   S.sent++;
+  /* ponyint_maybe_mute (actor.c:898-921): a send to an actor that is
+   * overloaded or muted (ponyint_triggers_muting, actor.c:1164-1169) mutes a
+   * sender that is not itself overloaded, unless it sends to itself. The
+   * sender stops after the message it is running (maybe_mute, actor.c:340-
+   * 367); the first such receiver is the one it waits on. */
+  if(S.n_trig && !S.cur_prev_o && to != S.cur && to < S.n_actors && S.trig[to] && !S.mute_hit)
+  {
+    S.mute_hit = 1;
+    S.mute_to = to;
+  }
   deliver(to, beh, arg);
 }
 
@@ -481,6 +530,8 @@ static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
       W(0) = (W(0) ^ arg) * 0x100000001b3ULL;
       if(seq != W(3 + slot) + 1) W(2) += 1;
       W(3 + slot) = seq;
+      /* param 1: yield after every k-th message (ponyint_actor_yield) */
+      if(t->params[1] && W(1) % t->params[1] == 0) S.yield_req = 1;
       break;
     }
   }
@@ -490,48 +541,109 @@ static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
 /* ---- run ----------------------------------------------------------------- */
 static uint64_t pending_total(void)
 {
-  uint64_t p = 0;
-  for(uint64_t a = 0; a < S.n_actors; a++)
-    p += S.mb[a].tail - S.mb[a].head;
-  return p;
+  return S.pending;
+}
+
+static void trig_set(uint64_t a, int v)
+{
+  if(S.trig[a] == (uint8_t)v) return;
+  S.trig[a] = (uint8_t)v;
+  if(v) S.n_trig++; else S.n_trig--;
+}
+
+/* One superstep, actors visited in id order (those with mail, muted or
+ * overloaded). Backpressure, restated for supersteps from actor.c:340-381,
+ * 449-471, 898-921 and scheduler.c:1496-1635:
+ *   - flags are read as the previous step left them;
+ *   - a muted actor stays muted (runs nothing, keeps its mail) while the
+ *     receiver it is muted on is overloaded; otherwise it is unmuted and runs
+ *     this step (Pony unmutes a receiver's senders when it clears OVERLOADED,
+ *     ponyint_actor_unsetoverloaded, actor.c:1121-1134; muted actors wait only
+ *     on overloaded ones, which always run, so muting cannot deadlock);
+ *   - an actor runs min(batch, mail at step start) messages and stops early
+ *     after a message whose sends muted it (send()) or that yielded
+ *     (ponyint_actor_yield, actor.c:675-679); the rest waits, in order;
+ *   - it is overloaded after the step iff it ran a full batch and was not
+ *     muted (batch_limit_reached, actor.c:369-381); an actor that did not run
+ *     is not overloaded. */
+static void run_step(void)
+{
+  typedef struct { uint64_t a; int t; } upd_t;
+  static upd_t* upd = NULL;
+  static uint64_t upd_alloc = 0;
+  uint64_t n_upd = 0;
+  S.running = 1;
+  const uint64_t words = (S.n_actors + 63) / 64;
+  for(uint64_t w = 0; w < words; w++)
+  {
+    uint64_t bits = S.live[w];
+    while(bits)
+    {
+      const uint64_t a = w * 64 + (uint64_t)__builtin_ctzll(bits);
+      bits &= bits - 1;
+      otype_t* t = &S.types[S.type_of[a]];
+      mbox_t* m = &S.mb[a];
+      oflag_t* f = &S.fl[a];
+      const int prev_o = f->o;
+      uint64_t handled = 0;
+      int muted_now = 0;
+      if(f->m && (S.trig[f->r] & 1u))
+        muted_now = 1;                 /* still waiting: nothing runs */
+      else
+      {
+        f->m = 0;
+        const uint64_t avail = (m->stamp == S.steps + 1 ? m->tail0 : m->tail) - m->head;
+        const uint64_t w_ = avail < t->batch ? avail : t->batch;
+        S.cur = a; S.cur_prev_o = prev_o; S.mute_hit = 0; S.yield_req = 0;
+        for(uint64_t k = 0; k < w_; k++)
+        {
+          orec_t r = m->buf[m->head % m->cap_alloc];
+          m->head++;
+          S.pending--;
+          t->delivered++;
+          S.delivered++;
+          handled++;
+          handle(t, a, r.beh, r.arg);
+          if(S.mute_hit || S.yield_req) break;
+        }
+        if(S.mute_hit) { muted_now = 1; f->r = (uint32_t)S.mute_to; }
+      }
+      f->m = (uint8_t)muted_now;
+      f->o = (uint8_t)(handled == t->batch && !muted_now);
+      if(n_upd == upd_alloc)
+      {
+        upd_alloc = upd_alloc ? 2 * upd_alloc : 1024;
+        upd = realloc(upd, upd_alloc * sizeof(upd_t));
+      }
+      upd[n_upd].a = a;
+      upd[n_upd].t = (int)f->o | ((int)f->m << 1);
+      n_upd++;
+    }
+  }
+  S.running = 0;
+  /* the next step reads the flags this one left */
+  for(uint64_t k = 0; k < n_upd; k++)
+  {
+    const uint64_t a = upd[k].a;
+    trig_set(a, upd[k].t);
+    if(S.mb[a].tail == S.mb[a].head && !S.fl[a].m && !S.fl[a].o)
+      S.live[a >> 6] &= ~(1ull << (a & 63));
+  }
 }
 
 int or_run(uint64_t max_steps, uint64_t* steps_done)
 {
   if(!S.init) return GPU_ACTOR_ESTATE;
   uint64_t done = 0;
-  uint64_t* avail = malloc((S.n_actors ? S.n_actors : 1) * sizeof(uint64_t));
-  if(!avail) return GPU_ACTOR_ENOMEM;
+  /* runs while mail is pending; flags left by the last step are honoured by
+   * the next run */
   while((max_steps == 0 || done < max_steps) && pending_total() > 0)
   {
-    for(uint64_t a = 0; a < S.n_actors; a++)
-    {
-      S.mb[a].head_start = S.mb[a].head;
-      avail[a] = S.mb[a].tail - S.mb[a].head;
-    }
-    for(uint64_t a = 0; a < S.n_actors; a++)
-    {
-      if(avail[a] == 0) continue;
-      otype_t* t = &S.types[S.type_of[a]];
-      uint64_t w = avail[a] < t->batch ? avail[a] : t->batch;
-      mbox_t* m = &S.mb[a];
-      for(uint64_t k = 0; k < w; k++)
-      {
-        orec_t r = m->buf[m->head % m->cap_alloc];
-        m->head++;
-        t->delivered++;
-        S.delivered++;
-        handle(t, a, r.beh, r.arg);
-      }
-    }
+    run_step();
     place_spawns();
-    /* the window for host sends after this step starts at the new head */
-    for(uint64_t a = 0; a < S.n_actors; a++)
-      S.mb[a].head_start = S.mb[a].head;
+    S.steps++;
     done++;
   }
-  free(avail);
-  S.steps += done;
   if(steps_done) *steps_done = done;
   return S.dropped ? GPU_ACTOR_EMAILBOX : 0;
 }

@@ -276,6 +276,19 @@ struct Engine {
     unsigned int pad;
     unsigned long long skipped;
   };
+  // backpressure: trigger bytes per global id and parity
+  // (d_trig_own: this rank's own bytes when n_ranks > 1, merged into d_trig),
+  // the receiver each muted local actor waits on, per-zone trigger counts,
+  // per-step counts (index = step mod 3), and the step index
+  uint8_t* d_trig[2] = {nullptr, nullptr};
+  uint8_t* d_trig_own[2] = {nullptr, nullptr};
+  uint64_t trig_bytes = 0;
+  bool trig_stale[2] = {false, false};
+  uint32_t* d_muted_on = nullptr;
+  uint64_t muted_on_cap = 0;
+  uint32_t* d_ztrig[2] = {nullptr, nullptr};
+  unsigned int* d_trig_n = nullptr;
+  uint32_t sidx = 0;
   SpillRec* d_spill[2] = {nullptr, nullptr};
   uint32_t spill_cap = 0;
   SpillStat* d_sstat = nullptr;
@@ -363,6 +376,14 @@ int upload_types()
   e.dbg = g.d_dbg;
   e.spawn_key = g.d_skey[0]; e.spawn_arg = g.d_sarg[0];
   e.spawn_n = g.d_spawn_n; e.spawn_cap = g.spawn_cap;
+  for(int p = 0; p < 2; ++p)
+  {
+    e.trig[p] = g.d_trig[p];
+    e.trig_own[p] = R() > 1 ? g.d_trig_own[p] : g.d_trig[p];
+    e.ztrig[p] = g.d_ztrig[p];
+  }
+  e.muted_on = g.d_muted_on;
+  e.trig_n = g.d_trig_n;
   e.spill[0] = g.d_spill[0]; e.spill[1] = g.d_spill[1];
   e.spill_n = g.d_sstat ? g.d_sstat->spill_n : nullptr;
   e.halt = g.d_sstat ? &g.d_sstat->halt : nullptr;
@@ -539,13 +560,30 @@ int relayout_zones()
   if(g.d_O) HIPCK(hipFree(g.d_O));
   if(g.d_zoff) HIPCK(hipFree(g.d_zoff));
   if(g.d_zcap) HIPCK(hipFree(g.d_zcap));
-  HIPCK(hipMalloc(&g.d_S, 2 * bytes));
+  HIPCK(hipMalloc(&g.d_S, 3 * bytes));     // 2 x: records of a zone; 1 x: sort scratch
   HIPCK(hipMalloc(&g.d_O, std::max<uint64_t>(total, 16) * sizeof(ORec)));
   g.d_zoff = d_off;
   g.d_zcap = d_cap;
   g.zone_records = total;
   g.n_zones = nz;
   g.zcap_host = cap;
+  // the receiver each muted actor waits on, one word per local slot
+  const uint64_t slots = (uint64_t)nz * kZone;
+  if(slots > g.muted_on_cap)
+  {
+    uint32_t* mo = nullptr;
+    HIPCK(hipMalloc(&mo, slots * sizeof(uint32_t)));
+    HIPCK(hipMemsetAsync(mo, 0, slots * sizeof(uint32_t), g.stream));
+    if(g.d_muted_on)
+    {
+      HIPCK(hipMemcpyAsync(mo, g.d_muted_on, g.muted_on_cap * sizeof(uint32_t),
+        hipMemcpyDeviceToDevice, g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+      HIPCK(hipFree(g.d_muted_on));
+    }
+    g.d_muted_on = mo;
+    g.muted_on_cap = slots;
+  }
   return ensure_spill(std::max<uint64_t>(1u << 20, total / 4));
 }
 
@@ -668,7 +706,7 @@ int exchange(uint32_t land_par)
 
 // k_step compiled for the one handler table all serial actors share, when
 // they do (smaller code, no spills); the any-mix instantiation otherwise.
-typedef void (*step_kernel_t)(uint32_t, uint32_t);
+typedef void (*step_kernel_t)(uint32_t, uint32_t, uint32_t);
 step_kernel_t pick_step_kernel()
 {
   int only = -1;
@@ -727,26 +765,73 @@ int spawn_process(uint32_t cur)
   return 0;
 }
 
+// n_ranks > 1: the count of actors that trigger muting after step `sidx`
+// (summed over ranks in place), and, when any do (or the merged bytes of this
+// parity were nonzero last time), every rank's own trigger bytes summed into
+// the global array the next step reads (each byte has one writer, so the sum
+// is the merge).
+int merge_triggers(uint32_t sidx)
+{
+  const uint32_t slot = (sidx + 1) % 3, p = g.par;
+  unsigned int cnt = 0;
+  if(g.xp_ar)
+  {
+    HIPCK(hipMemcpyAsync(&cnt, g.d_trig_n + slot, sizeof(cnt), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    uint64_t c64 = cnt;
+    if(g.xp_ar(g.xp_ctx, &c64, 1) != 0) return GPU_ACTOR_ECOMM;
+    cnt = (unsigned int)c64;
+    HIPCK(hipMemcpyAsync(g.d_trig_n + slot, &cnt, sizeof(cnt), hipMemcpyHostToDevice, g.stream));
+    if(cnt || g.trig_stale[p])
+    {
+      std::vector<uint64_t> h(g.trig_bytes / 8);
+      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[p], g.trig_bytes, hipMemcpyDeviceToHost, g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+      if(g.xp_ar(g.xp_ctx, h.data(), h.size()) != 0) return GPU_ACTOR_ECOMM;
+      HIPCK(hipMemcpyAsync(g.d_trig[p], h.data(), g.trig_bytes, hipMemcpyHostToDevice, g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+    }
+  }
+  else
+  {
+    NCCLCK(ncclAllReduce(g.d_trig_n + slot, g.d_trig_n + slot, 1, ncclUint32, ncclSum, g.comm,
+      g.stream));
+    HIPCK(hipMemcpyAsync(&cnt, g.d_trig_n + slot, sizeof(cnt), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    if(cnt || g.trig_stale[p])
+      NCCLCK(ncclAllReduce(g.d_trig_own[p], g.d_trig[p], g.trig_bytes, ncclUint8, ncclSum, g.comm,
+        g.stream));
+  }
+  g.trig_stale[p] = cnt != 0;
+  return 0;
+}
+
 // One superstep: k_step on parity g.par (+ exchange), then flip parity.
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
-  const size_t dyn = 4 * sizeof(uint32_t) * (g.n_zones + (R() > 1 ? R() : 0));
+  // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
+  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
+                                                          kSortWork);
   step_kernel_t kern = pick_step_kernel();
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
     hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), (uint32_t)dyn, g.stream,
-      e0, e1, 0u, g.par, slot);
+      e0, e1, 0u, g.par, slot, g.sidx);
   }
   else
-    hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot);
+    hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot, g.sidx);
   HIPCK(hipGetLastError());
+  const uint32_t step_sidx = g.sidx;
   g.par ^= 1u;
+  g.sidx++;
   if(R() > 1)
   {
     int rc = exchange(g.par);
+    if(rc) return rc;
+    rc = merge_triggers(step_sidx);
     if(rc) return rc;
     // steps never halt on the device with n_ranks > 1 (ranks would part
     // ways): a zone that overflowed is grown before the next step
@@ -832,6 +917,14 @@ void free_all()
   if(g.d_sstat) (void)hipFree(g.d_sstat);
   if(g.h_sstat) (void)hipHostFree(g.h_sstat);
   if(g.d_need) (void)hipFree(g.d_need);
+  for(int p = 0; p < 2; ++p)
+  {
+    if(g.d_trig[p]) (void)hipFree(g.d_trig[p]);
+    if(g.d_trig_own[p]) (void)hipFree(g.d_trig_own[p]);
+    if(g.d_ztrig[p]) (void)hipFree(g.d_ztrig[p]);
+  }
+  if(g.d_muted_on) (void)hipFree(g.d_muted_on);
+  if(g.d_trig_n) (void)hipFree(g.d_trig_n);
   if(g.h_ctl) (void)hipHostFree(g.h_ctl);
   if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
@@ -973,6 +1066,21 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipHostMalloc(&g.h_sstat, sizeof(Engine::SpillStat), hipHostMallocDefault));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   HIPCK(hipMalloc(&g.d_need, kMaxZones * sizeof(uint32_t)));
+  g.trig_bytes = (g.cfg.max_actors + 2 * kZone + 7) & ~7ull;
+  for(int p = 0; p < 2; ++p)
+  {
+    HIPCK(hipMalloc(&g.d_trig[p], g.trig_bytes));
+    HIPCK(hipMemsetAsync(g.d_trig[p], 0, g.trig_bytes, g.stream));
+    HIPCK(hipMalloc(&g.d_ztrig[p], kMaxZones * sizeof(uint32_t)));
+    HIPCK(hipMemsetAsync(g.d_ztrig[p], 0, kMaxZones * sizeof(uint32_t), g.stream));
+    if(R() > 1)
+    {
+      HIPCK(hipMalloc(&g.d_trig_own[p], g.trig_bytes));
+      HIPCK(hipMemsetAsync(g.d_trig_own[p], 0, g.trig_bytes, g.stream));
+    }
+  }
+  HIPCK(hipMalloc(&g.d_trig_n, 4 * sizeof(unsigned int)));
+  HIPCK(hipMemsetAsync(g.d_trig_n, 0, 4 * sizeof(unsigned int), g.stream));
   HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
   HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
@@ -1050,6 +1158,13 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
   g.d_spill[0] = g.d_spill[1] = nullptr; g.spill_cap = 0; g.d_sstat = nullptr; g.h_sstat = nullptr;
   g.d_need = nullptr; g.zcap_min.clear(); g.zcap_host.clear(); g.fixups = 0;
+  for(int p = 0; p < 2; ++p)
+  {
+    g.d_trig[p] = g.d_trig_own[p] = nullptr;
+    g.d_ztrig[p] = nullptr;
+    g.trig_stale[p] = false;
+  }
+  g.trig_bytes = 0; g.d_muted_on = nullptr; g.muted_on_cap = 0; g.d_trig_n = nullptr; g.sidx = 0;
   g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;
   for(int p = 0; p < 2; ++p) g.d_skey[p] = g.d_sarg[p] = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
@@ -1254,7 +1369,7 @@ bool sparse_ok()
 int run_sparse(uint64_t max_steps, SparseCtl& out)
 {
   hipLaunchKernelGGL(k_sparse, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
-    (unsigned long long)max_steps, g.d_ctl);
+    (unsigned long long)max_steps, g.d_ctl, g.sidx);
   HIPCK(hipGetLastError());
   HIPCK(hipMemcpyAsync(g.h_ctl, g.d_ctl, sizeof(SparseCtl), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
@@ -1262,6 +1377,7 @@ int run_sparse(uint64_t max_steps, SparseCtl& out)
   HIPCK(hipStreamSynchronize(g.stream));
   out = *g.h_ctl;
   g.par = out.par;
+  g.sidx += (uint32_t)out.steps;
   g.sparse_launches++;
   g.sparse_steps += out.steps;
   return 0;
@@ -1303,7 +1419,7 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
     rc = pending_now(before);
     if(rc) return rc;
     std::vector<unsigned long long> pv;
-    std::vector<uint32_t> par_at(kChunk + 1);
+    std::vector<uint32_t> par_at(kChunk + 1), sidx_at(kChunk + 1);
     const bool sp = sparse_ok();
     while(before > 0 && (max_steps == 0 || done < max_steps))
     {
@@ -1342,6 +1458,7 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       for(uint32_t j = 0; j < k; ++j)
       {
         par_at[j] = g.par;
+        sidx_at[j] = g.sidx;
         rc = launch_step(j, nullptr, nullptr);
         if(rc) return rc;
       }
@@ -1363,7 +1480,7 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       if(halted || spill_pending())
       {
         // steps from j on did not run: resume at the parity step j would have read
-        if(halted) g.par = par_at[j];
+        if(halted) { g.par = par_at[j]; g.sidx = sidx_at[j]; }
         rc = fixup_spill();
         if(rc) return rc;
         rc = pending_now(before);
@@ -1472,7 +1589,7 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   while(left)
   {
     HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-    const uint32_t par0 = g.par;
+    const uint32_t par0 = g.par, sidx0 = g.sidx;
     HIPCK(hipEventRecord(g.ev[0], g.stream));
     for(uint64_t j = 0; j < left; ++j)
     {
@@ -1489,7 +1606,11 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
     // steps after an overflow did not run (one rank): grow, then run them
     const uint64_t skipped = std::min<uint64_t>(g.h_sstat->skipped, left);
     const uint64_t ran = left - skipped;
-    if(R() == 1 && skipped) g.par = par0 ^ (uint32_t)(ran & 1u);
+    if(R() == 1 && skipped)
+    {
+      g.par = par0 ^ (uint32_t)(ran & 1u);
+      g.sidx = sidx0 + (uint32_t)ran;
+    }
     rc = fixup_spill();
     if(rc) return rc;
     left = skipped;

@@ -117,7 +117,7 @@ struct EngDev {
   ZRec* carry[2];
   uint32_t* land_n[2];            // [n_zones]
   uint32_t* carry_n[2];
-  ZRec* S;                        // zone z: [2 zoff[z], 2 zoff[z] + 2 zcapz[z])
+  ZRec* S;                        // zone z: [3 zoff[z], 3 zoff[z] + 3 zcapz[z])
   ORec* O;                        // zone z: [zoff[z], zoff[z] + zcapz[z])
   unsigned long long* stats;
   unsigned long long* pend;       // per-step pending counters
@@ -135,6 +135,18 @@ struct EngDev {
   // zone buffers past capacity (never dropped): spill[p] holds the records
   // for parity p's landing/carry buffers; a step that finds spill_n[cur] or
   // halt set does not run (one rank) until the host has grown the zones
+  // backpressure (Pony's mute, restated per superstep): per
+  // global id, the state the last step left, bit 0 overloaded, bit 1 muted
+  // (trig[p] is read by senders in the step that reads parity p; with
+  // n_ranks > 1 each rank writes its own actors into trig_own[p] and the
+  // host merges them into trig[p]); per local slot the receiver a muted actor
+  // waits on; per zone how many of its actors have a nonzero byte in trig[p];
+  // per step (index mod 3) how many actors trigger muting
+  uint8_t* trig[2];
+  uint8_t* trig_own[2];
+  uint32_t* muted_on;
+  uint32_t* ztrig[2];
+  unsigned int* trig_n;           // [3]
   SpillRec* spill[2];
   unsigned int* spill_n;          // [2]
   unsigned int* halt;             // set by a skipped step: every later step skips too
@@ -221,9 +233,18 @@ struct ActorBase {
   uint32_t rc_first, rc_count, rc_lfirst, rc_lcount;
   uint64_t* rc_state;
   uint64_t rc_mask;
+  // backpressure while this actor runs: the step's trigger bytes (null when
+  // no actor triggers muting), whether this actor was overloaded after the
+  // last step, and what its sends and behaviours asked for
+  const uint8_t* trig;
+  uint32_t prev_o;
+  uint32_t mute_hit;     // a send went to an overloaded or muted actor
+  uint32_t mute_to;      // the first such receiver
+  uint32_t yield_req;    // the behaviour yielded (ponyint_actor_yield)
 
   __device__ __forceinline__ void reset_common()
   {
+    trig = nullptr; prev_o = 0; mute_hit = 0; mute_to = 0; yield_req = 0;
     seq = 0; sent = 0; applied = 0; applied_type = -1;
     fan = nullptr; fan_t = -1;
     rc_first = rc_count = rc_lfirst = rc_lcount = 0;
@@ -352,6 +373,22 @@ __device__ __forceinline__ void send_serial(A& a, uint32_t to, uint32_t beh, uin
   }
   a.put(to, (a.seq << 16) | (beh << 12), arg);
   a.seq++;
+  // ponyint_maybe_mute (actor.c:898-921): a send to an actor that is
+  // overloaded or muted mutes a sender that is not overloaded itself, unless
+  // it sends to itself; the sender stops after the behaviour it is running
+  if(a.trig && !a.prev_o && !a.mute_hit && to != a.self && a.trig[to] != 0)
+  {
+    a.mute_hit = 1;
+    a.mute_to = to;
+  }
+}
+
+// ponyint_actor_yield (actor.c:675-679): end the actor's run after this
+// behaviour; the rest of its mail waits for the next step.
+template <class A>
+__device__ __forceinline__ void actor_yield(A& a)
+{
+  a.yield_req = 1;
 }
 
 // pony_create inside a behaviour + its constructor message (actor.c:688-734,
@@ -620,6 +657,8 @@ __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SINK>, const Type
   if(seq != last + 1) s[2] += 1;
 #pragma unroll
   for(int k = 0; k < 8; ++k) s[3 + k] = (slot == (uint32_t)k) ? seq : s[3 + k];
+  // param 1: yield after every k-th message
+  if(T.params[1] && s[1] % T.params[1] == 0) actor_yield(a);
 }
 
 // examples/spreader/main.pony:9-48

@@ -170,7 +170,7 @@ __device__ __forceinline__ uint32_t sp_block_excl_scan(uint32_t v, uint32_t* s_t
 // Runs up to max_steps supersteps (0: no limit) starting from the records in
 // landing[cur]; R == 1 and no spawning types (the host checks).
 __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned long long max_steps,
-  SparseCtl* ctl)
+  SparseCtl* ctl, uint32_t sidx)
 {
   __shared__ uint64_t bK[3][kSpCap], bA[3][kSpCap];
   __shared__ uint32_t bW[3][kSpCap];
@@ -193,7 +193,9 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     s_tinfo[tid].lfirst = T.lfirst;
     s_tinfo[tid].lcount = T.lcount;
     s_tinfo[tid].batch = T.batch;
-    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER) ? kSpNoRun : 0u;
+    // reducible types never run; spawning and yielding ones need the zone path
+    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER ||
+                          (T.ht == GPU_ACTOR_HT_FIFO_SINK && T.params[1] != 0)) ? kSpNoRun : 0u;
   }
   if(tid == 0) { sp_cnt[0] = 0; sp_cnt[1] = 0; s_over = 0; }
   s_acc[tid] = 0;
@@ -215,7 +217,10 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
   uint32_t run = sp_block_excl_scan(mine, s_tmp, total);
   for(uint32_t z = z0; z < z1; ++z) { const uint32_t c = s_zpre[z]; s_zpre[z] = run; run += c; }
   if(tid == 0) s_zpre[nz] = total;
-  const bool pending_fixup = c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u;
+  // spilled records wait for the host; an actor that triggers muting
+  // (overloaded or muted) needs the zone path's backpressure
+  const bool pending_fixup = c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u ||
+                             c_eng.trig_n[sidx % 3u] != 0u;
   if(__syncthreads_or(carried) || total > kSpCap || pending_fixup)
   {
     // the dense path owns this step: nothing was touched
@@ -235,6 +240,16 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     bA[0][i] = ((uint64_t)v.w << 32) | v.z;
   }
   for(uint32_t z = z0; z < z1; ++z) c_eng.land_n[cur][z] = 0;
+  // no actor triggers muting now; bytes a zone left in the other parity two
+  // steps ago are cleared, so both parities read as all-quiet when the zone
+  // path resumes
+  for(uint32_t z = z0; z < z1; ++z)
+    if(c_eng.ztrig[cur ^ 1u][z])
+    {
+      const uint32_t L0 = z * kZone, nact = min(kZone, c_eng.n_local - L0);
+      for(uint32_t i = 0; i < nact; ++i) c_eng.trig_own[cur ^ 1u][L0 + i] = 0;
+      c_eng.ztrig[cur ^ 1u][z] = 0;
+    }
   __syncthreads();
 
   // ---- supersteps --------------------------------------------------------------------
@@ -321,7 +336,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       {
         h_r = r; h_g = same;
         const int t = sp_type(s_tinfo, n_types, (uint32_t)(Acur.K[tid] >> 32));
-        if(t < 0 || (s_tinfo[t].flags & kSpNoRun) || same > s_tinfo[t].batch) dense = 1;
+        // a full batch would leave the actor overloaded: the zone path owns that
+        if(t < 0 || (s_tinfo[t].flags & kSpNoRun) || same >= s_tinfo[t].batch) dense = 1;
       }
     }
     s_acc[tid] = 0;                          // ready for the next step's counts
@@ -409,6 +425,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     for(int k = 0; k < 4; ++k) c_eng.dbg[k] = ph[k];
 #endif
 #undef SP_STAMP
+  if(tid < 3) c_eng.trig_n[tid] = 0;       // nothing triggers after sparse steps
   if(tid == 0)
   {
     ctl->steps = steps;

@@ -255,17 +255,25 @@ struct AccS {
   }
 };
 
-// Drain one actor: handle min(batch, n) messages — carried mail, then the
-// arrival group in (from, seq) key order — and hand the canonical tail to the
-// next step's carry buffer.
+template <int HT> __host__ __device__ constexpr bool may_yield()
+{
+  return HT == GPU_ACTOR_HT_FIFO_SINK;
+}
+
+// Drain one actor: handle up to min(batch, n) messages — carried mail, then
+// the arrival group in (from, seq) key order — stopping early after a
+// behaviour whose sends muted the actor or that yielded. Returns how many ran;
+// the rest, [done, n) of acc, is left in canonical order for the carry-out
+// pass (the group is sorted in place when it was not handled whole).
 template <int HT, class Acc>
 __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, Acc acc,
-  uint32_t n, uint32_t nc, uint32_t z, uint32_t co)
+  uint32_t n, uint32_t nc, bool presorted)
 {
   // a register copy of the type's fields: read once, not re-read after every
   // store the handlers make (the compiler cannot prove they do not alias)
   const TypeDev T = Tref;
   constexpr int NW = HT_Words<HT>::W;
+  constexpr bool kY = may_yield<HT>();
   const uint32_t w = n < T.batch ? n : T.batch;
   uint64_t s[NW];
 #pragma unroll
@@ -273,7 +281,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   const uint32_t g = n - nc;
   const uint32_t hc = min(w, nc);                 // carried messages handled now
   constexpr uint32_t SM = small_regs<HT>();
-  const bool small = g > 0 && w - hc >= g && g <= SM;
+  const bool small = g > 0 && w - hc >= g && g <= SM && !presorted;
   // small arrival group: its records are loaded with the state, before any
   // handler runs (one round of memory latency for the actor); the behaviour
   // rides in the key's low bits (key << 4 | beh sorts like the key)
@@ -296,19 +304,21 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   // message made (vmcnt counts stores too).
   __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
   uint32_t done = 0;
-  while(done < hc)
+  bool stop = false, sorted = false;
+  while(done < hc && !stop)
   {
     const ZRec r = acc.rec(done);
     handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
     ++done;
+    stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
   }
-  if(g > 0)
+  if(g > 0 && !stop)
   {
     const uint32_t q = w - done;
     if(small)
     {
       // small group handled whole: all records in registers, select by key
-      for(uint32_t r = 0; r < g; ++r)
+      for(uint32_t r = 0; r < g && !stop; ++r)
       {
         uint64_t best = k[0], barg = v[0];
         uint32_t bi = 0;
@@ -319,14 +329,15 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
         for(int j = 0; j < (int)SM; ++j)
           if((uint32_t)j == bi) k[j] = ~0ull;
         handle(HtTag<HT>{}, T, a, s, (uint32_t)best & 0xFu, barg);
+        ++done;
+        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
-      done += g;
     }
-    else if(q >= g)
+    else if(q >= g && !presorted)
     {
       // large group handled whole: select in key order
       uint64_t last = 0;
-      for(uint32_t r = 0; r < g; ++r)
+      for(uint32_t r = 0; r < g && !stop; ++r)
       {
         uint64_t best = ~0ull;
         uint32_t bi = 0;
@@ -338,26 +349,41 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
         const ZRec rr = acc.rec(nc + bi);
         handle(HtTag<HT>{}, T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg);
         last = best;
+        ++done;
+        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
-      done += g;
     }
     else
     {
-      // part of the group carries over: canonicalise it first
-      acc.sort(nc, g);
-      for(uint32_t k = 0; k < q; ++k)
+      // part of the group carries over (or it was sorted by the whole
+      // workgroup already): canonical order first
+      if(!presorted) acc.sort(nc, g);
+      sorted = true;
+      for(uint32_t k = 0; k < q && !stop; ++k)
       {
         const ZRec r = acc.rec(nc + k);
         handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
+        ++done;
+        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
-      done += q;
     }
   }
 #pragma unroll
   for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = s[k];
-  // the unhandled tail, canonical, becomes next step's carried mail (its
-  // positions run past the zone's capacity into the spill list, never lost)
-  ZRec* cout = c_eng.carry[a.nxt] + c_eng.zoff[z];
+  // what ran of the group were its smallest keys: sorted, the group's tail
+  // is the canonical remainder
+  if(done < n && g > 1 && !sorted && !presorted) acc.sort(nc, g);
+  return done;
+}
+
+// The unhandled tail [done, n) of an actor's segment, already canonical, to
+// the next step's carry buffer at carry position co (positions past the
+// zone's capacity go to the spill list: never lost).
+template <class Acc>
+__device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, uint32_t z,
+  uint32_t co, uint32_t nxt)
+{
+  ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
   const uint32_t cap = zone_capacity(z);
   for(uint32_t k = done; k < n; ++k)
   {
@@ -368,16 +394,165 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
     if(pos < cap)
       *reinterpret_cast<uint4*>(cout + pos) = u;
     else
-      spill_rec(a.nxt, kSpillCarry, z, pos, u);
+      spill_rec(nxt, kSpillCarry, z, pos, u);
   }
-  return done;
+}
+
+// ---- hot receivers: arrival groups sorted by the whole workgroup ------------------
+// An actor with more than kBigGroup arrivals in one step (fan-in to a
+// non-commutative receiver) would otherwise order them inside its own lane,
+// O(g^2). Instead, before the behaviours run, the workgroup sorts each such
+// group with a stable LSD radix sort (8-bit digits) over u64 items
+// key << kPayBits | payload, the key compressed to (from - min from) << sbits
+// | seq, the payload the record's idx entry (or its position in S).
+constexpr uint32_t kBigGroup = 128;
+constexpr uint32_t kMaxBig = 32;            // big groups sorted per round of the loop
+constexpr uint32_t kPayBits = 20;           // payload bits of an item (group <= 2^20)
+constexpr uint32_t kSortWork = 256 + kZoneWaves * 256;   // u32 of LDS the sort borrows
+
+// Stable sort of n items in a by item bits [lo, hi); b is scratch of n items.
+// The result ends in a. All threads call; ends behind a barrier.
+__device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t hi,
+  uint32_t* s_work)
+{
+  uint32_t* s_bin = s_work;                // [256] running base of each digit
+  uint32_t* s_wc = s_work + 256;           // [kZoneWaves][256] this tile's counts per wave
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t* src = a;
+  uint64_t* dst = b;
+  for(uint32_t sh = lo; sh < hi; sh += 8)
+  {
+    for(uint32_t d = tid; d < 256; d += kZoneThreads) s_bin[d] = 0;
+    __syncthreads();
+    for(uint32_t i = tid; i < n; i += kZoneThreads) atomicAdd(&s_bin[(src[i] >> sh) & 255u], 1u);
+    __syncthreads();
+    if(wv == 0)
+    {
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for(int k = 0; k < 4; ++k) { v[k] = s_bin[lane * 4 + k]; sum += v[k]; }
+      uint32_t run = wave_incl_scan(sum, lane) - sum;
+#pragma unroll
+      for(int k = 0; k < 4; ++k) { s_bin[lane * 4 + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    for(uint32_t t0 = 0; t0 < n; t0 += kZoneThreads)
+    {
+      const uint32_t i = t0 + tid;
+      const bool valid = i < n;
+      const uint64_t x = valid ? src[i] : 0ull;
+      const uint32_t d = (uint32_t)(x >> sh) & 255u;
+      // lanes of this wave holding the same digit: 8 ballots
+      uint64_t same = __ballot(valid);
+#pragma unroll
+      for(int bit = 0; bit < 8; ++bit)
+      {
+        const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
+        same &= ((d >> bit) & 1u) ? bb : ~bb;
+      }
+      for(uint32_t k = lane; k < 256; k += 64) s_wc[wv * 256 + k] = 0;
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t rank = __popcll(same & lt);
+      if(valid && rank == 0) s_wc[wv * 256 + d] = __popcll(same);
+      __syncthreads();
+      if(valid)
+      {
+        uint32_t pre = s_bin[d];
+        for(uint32_t w = 0; w < wv; ++w) pre += s_wc[w * 256 + d];
+        dst[pre + rank] = x;
+      }
+      __syncthreads();
+      for(uint32_t k = tid; k < 256; k += kZoneThreads)
+      {
+        uint32_t c = 0;
+        for(uint32_t w = 0; w < (uint32_t)kZoneWaves; ++w) c += s_wc[w * 256 + k];
+        s_bin[k] += c;
+      }
+      __syncthreads();
+    }
+    uint64_t* t = src; src = dst; dst = t;
+  }
+  if(src != a)
+  {
+    for(uint32_t i = tid; i < n; i += kZoneThreads) a[i] = src[i];
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint32_t bits_for(uint32_t v)
+{
+  return v ? 32u - (uint32_t)__clz(v) : 0u;
+}
+
+// Sort the arrival group [nc, nc + g) of one actor's segment, by the whole
+// workgroup. idx path: payload = the idx entry; S path: payload = position,
+// and the records are permuted through scratch `tmp` (g records). Returns
+// false (nothing changed) when the compressed key does not fit.
+template <class Acc>
+__device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, uint32_t g,
+  uint64_t* ia, uint64_t* ib, ZRec* tmp, uint32_t* s_work, uint32_t* s_red3)
+{
+  const uint32_t tid = threadIdx.x;
+  // key range: min/max sender, max sequence
+  uint32_t fmin = 0xFFFFFFFFu, fmax = 0, smax = 0;
+  for(uint32_t j = tid; j < g; j += kZoneThreads)
+  {
+    const ZRec r = acc.rec(nc + j);
+    fmin = min(fmin, r.from); fmax = max(fmax, r.from); smax = max(smax, r.w0 >> 16);
+  }
+  if(tid < 3) s_red3[tid] = tid == 0 ? 0xFFFFFFFFu : 0u;
+  __syncthreads();
+  atomicMin(&s_red3[0], fmin); atomicMax(&s_red3[1], fmax); atomicMax(&s_red3[2], smax);
+  __syncthreads();
+  fmin = s_red3[0]; fmax = s_red3[1]; smax = s_red3[2];
+  __syncthreads();
+  const uint32_t sbits = bits_for(smax), kbits = bits_for(fmax - fmin) + sbits;
+  const uint32_t pay = idx ? 16u : kPayBits;
+  if(kbits + pay > 64u) return false;
+  for(uint32_t j = tid; j < g; j += kZoneThreads)
+  {
+    const ZRec r = acc.rec(nc + j);
+    const uint64_t key = ((uint64_t)(r.from - fmin) << sbits) | (r.w0 >> 16);
+    ia[j] = (key << pay) | (idx ? (uint64_t)idx[nc + j] : (uint64_t)j);
+  }
+  __syncthreads();
+  coop_radix_sort(ia, ib, g, pay, pay + ((kbits + 7u) & ~7u), s_work);
+  const uint64_t pm = (1ull << pay) - 1;
+  if(idx)
+  {
+    for(uint32_t j = tid; j < g; j += kZoneThreads) idx[nc + j] = (uint16_t)(ia[j] & pm);
+  }
+  else
+  {
+    for(uint32_t j = tid; j < g; j += kZoneThreads) tmp[j] = seg[nc + (uint32_t)(ia[j] & pm)];
+    __syncthreads();
+    for(uint32_t j = tid; j < g; j += kZoneThreads) seg[nc + j] = tmp[j];
+  }
+  __syncthreads();
+  return true;
+}
+
+// One actor of the zone: stays muted (nothing runs; its arrivals are put in
+// canonical order for the carry) or drains.
+template <int HT, class Acc>
+__device__ __forceinline__ uint32_t zone_actor(const TypeDev& T, ZoneCtx& a, Acc acc, uint32_t n,
+  uint32_t nc, bool stays, bool presorted)
+{
+  if(stays)
+  {
+    if(n - nc > 1 && !presorted) acc.sort(nc, n - nc);
+    return 0;
+  }
+  return drain_zone<HT>(T, a, acc, n, nc, presorted);
 }
 
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
 // HTS >= 0: every serial actor of this engine runs handler table HTS (the host
 // checks), so only that table is compiled in; HTS < 0: any mix of tables.
 template <int HTS>
-__global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot)
+__global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
+  uint32_t sidx)
 {
   // 64 KB pool. Phases 1-3: per-actor arrays + the segment index; phase 4:
   // the outbox sort tile (kTile records).
@@ -396,6 +571,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tb[kZone];   // trigger byte per actor
+  __shared__ uint32_t s_ntrig;
+  __shared__ uint32_t s_bigbits[kZone / 32];   // groups the workgroup sorted this step
+  __shared__ uint32_t s_red3[3];
   constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
@@ -427,23 +606,45 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   uint32_t* s_hist = s_dyn;
   uint32_t* s_base = s_dyn + nb;
 
+  // Backpressure bookkeeping: ztc = this zone's actors that
+  // trigger muting after the last step (overloaded or muted); ztn = nonzero
+  // bytes this zone left in trig_own[nxt] two steps ago. trig_n is indexed by
+  // step mod 3: read this step's, add to the next's, clear the one after.
+  const uint32_t ztc = c_eng.ztrig[cur][z];
+  const uint32_t ztn = c_eng.ztrig[nxt][z];
+  const bool gate = c_eng.trig_n[sidx % 3u] != 0u;
+  if(z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+  uint8_t* const tb_out = c_eng.trig_own[nxt];
+
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
   for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
-  if(tid == 0) s_nout = 0;
+  if(tid == 0) { s_nout = 0; s_ntrig = 0; }
   __syncthreads();
   GPA_STAMP(0);
 
   // ---- 1. count --------------------------------------------------------------
   const uint32_t nc = min(c_eng.carry_n[cur][z], cap);
   const uint32_t nl = min(c_eng.land_n[cur][z], cap);
-  if(nc + nl == 0)
+  if(nc + nl == 0 && ztc == 0)
   {
     // an idle zone (uniform: every thread read the same counters) has
     // nothing to count, run or send — the quiet tail of a run, or zones of
-    // a sparse workload
+    // a sparse workload; it only clears trigger bytes it left two steps ago
     if(tid == 0) c_eng.carry_n[nxt][z] = 0;
+    if(ztn)
+    {
+      for(uint32_t i = tid; i < nact; i += kZoneThreads) tb_out[(L0 + i) * R + me] = 0;
+      if(tid == 0) c_eng.ztrig[nxt][z] = 0;
+    }
     return;
   }
+  // the trigger bytes of this zone's actors as the last step left them
+  if(ztc)
+    for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+      s_tb[i] = i < nact ? c_eng.trig[cur][(L0 + i) * R + me] : (uint8_t)0;
+  else
+    for(uint32_t i = tid; i < kZone / 4; i += kZoneThreads)
+      reinterpret_cast<uint32_t*>(s_tb)[i] = 0;
   const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
   const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
   const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
@@ -497,7 +698,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(2);
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
-  ZRec* Sz = c_eng.S + 2 * c_eng.zoff[z];
+  ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
   for(uint32_t i = tid; i < nc; i += kZoneThreads)
   {
     const ZRec r = C[i];
@@ -549,6 +750,49 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __syncthreads();
   GPA_STAMP(3);
 
+  // Hot receivers: groups above kBigGroup sorted by the whole workgroup
+  // (s_bigbits marks them for drain_zone). The sort borrows s_dyn, which the
+  // behaviours' bucket counts use next, and the zone's outbox / S scratch.
+  for(uint32_t k = tid; k < kZone / 32; k += kZoneThreads) s_bigbits[k] = 0;
+  {
+    int any_big = 0;
+    for(uint32_t i = tid; i < nact; i += kZoneThreads)
+      any_big |= (s_cnt[i] - s_ccnt[i]) > kBigGroup;
+    if(__syncthreads_or(any_big))
+    {
+      uint64_t* ia = reinterpret_cast<uint64_t*>(c_eng.O + c_eng.zoff[z]);
+      for(uint32_t i0 = 0; i0 < nact; )
+      {
+        // the next actor (in slot order) with a big group: found by scanning
+        if(tid == 0)
+        {
+          uint32_t i = i0;
+          while(i < nact && (s_cnt[i] - s_ccnt[i]) <= kBigGroup) ++i;
+          s_tmp[kZoneWaves] = i;
+        }
+        __syncthreads();
+        const uint32_t i = s_tmp[kZoneWaves];
+        __syncthreads();
+        if(i >= nact) break;
+        const uint32_t g = s_cnt[i] - s_ccnt[i];
+        bool ok;
+        if(use_idx)
+          ok = coop_sort_group(AccIdx{s_idx + s_off[i], C, Ld, nc}, s_idx + s_off[i], nullptr,
+                               s_ccnt[i], g, ia, ia + g, nullptr, s_dyn, s_red3);
+        else
+          ok = coop_sort_group(AccS{Sz + s_off[i]}, nullptr, Sz + s_off[i], s_ccnt[i], g, ia,
+                               ia + g, Sz + 2 * cap, s_dyn, s_red3);
+        if(ok && tid == 0) s_bigbits[i >> 5] |= 1u << (i & 31);
+        i0 = i + 1;
+      }
+      for(uint32_t b = tid; b < max(nb, kSortWork); b += kZoneThreads) s_dyn[b] = 0;
+      __syncthreads();
+    }
+  }
+  auto big_sorted = [&](uint32_t i) __attribute__((always_inline)) {
+    return ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
+  };
+
   // The zone's type when one type covers all of its slots, else -1. It is
   // wave-uniform, so that type's fields (batch, state, params) come through
   // scalar loads instead of a per-lane lookup chain.
@@ -558,31 +802,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       tz = (int)t;
   tz = __builtin_amdgcn_readfirstlane(tz);
 
-  // carry-out sizes (known before any handler runs) -> offsets
-  const uint32_t zbatch = tz >= 0 ? c_types[tz].batch : 0u;
+  // s_aux will hold each actor's unhandled remainder (known after it ran)
+  for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   int any_rem = 0;
-  for(uint32_t i = tid; i < kZone; i += kZoneThreads)
-  {
-    uint32_t rem = 0;
-    const uint32_t n = s_cnt[i];
-    if(i < nact && n)
-    {
-      uint32_t bt = zbatch;
-      if(tz < 0)
-      {
-        const int t = type_of_local(L0 + i);
-        bt = t >= 0 ? c_types[t].batch : ~0u;
-      }
-      rem = n > bt ? n - bt : 0u;
-    }
-    s_aux[i] = rem;
-    any_rem |= rem != 0u;
-  }
-  // no actor over its batch (the usual step): s_aux is all zeros, which is
-  // already its own exclusive scan
-  const uint32_t ncout = __syncthreads_or(any_rem) ? block_scan_zone(s_aux, s_tmp) : 0u;
-  if(tid == 0)
-    c_eng.carry_n[nxt][z] = ncout;          // past cap: the tail is in the spill list
 
   // ---- 3. run handlers -------------------------------------------------------------
   ZoneCtx a;
@@ -602,6 +824,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
   uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
   // drain local actor i, of type t (T = c_types[t])
+  uint8_t* const trig_cur = gate ? c_eng.trig[cur] : nullptr;
   auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
     const uint32_t n = s_cnt[i];
     const uint32_t L = L0 + i;
@@ -610,16 +833,24 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     a.src_local = i;
     a.type = t;
     a.seq = 0;
-    const uint32_t co = s_aux[i];
+    // backpressure: as the last step left this actor (bit 0 overloaded, bit
+    // 1 muted); a muted actor waits while the receiver it is muted on is
+    // overloaded (the release of ponyint_actor_unsetoverloaded, actor.c:1121)
+    const uint32_t tb = s_tb[i];
+    a.trig = trig_cur;
+    a.prev_o = tb & 1u;
+    a.mute_hit = 0;
+    a.yield_req = 0;
+    const bool stays = (tb & 2u) && (c_eng.trig[cur][c_eng.muted_on[L]] & 1u);
     uint32_t d = 0;
 #define ZDRAIN(HT)                                                                    \
     if(use_idx)                                                                       \
     {                                                                                 \
       AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                        \
-      d = drain_zone<HT>(T, a, acc, n, s_ccnt[i], z, co);                              \
+      d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
     }                                                                                 \
     else                                                                              \
-      d = drain_zone<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], z, co);
+      d = zone_actor<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], stays, big_sorted(i));
     if constexpr(HTS >= 0)
     {
       ZDRAIN(HTS)
@@ -643,6 +874,16 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
     }
 #undef ZDRAIN
+    // overloaded iff a full batch ran and the actor was not muted
+    // (batch_limit_reached, actor.c:369-381; maybe_mute first, 449-460)
+    const uint32_t o = (d == T.batch && !a.mute_hit) ? 1u : 0u;
+    const uint32_t m = (stays || a.mute_hit) ? 1u : 0u;
+    if(a.mute_hit) c_eng.muted_on[L] = a.mute_to;
+    const uint32_t nb_ = o | (m << 1);
+    s_tb[i] = (uint8_t)nb_;
+    if(nb_) atomicAdd(&s_ntrig, 1u);
+    s_aux[i] = n - d;
+    any_rem |= (n - d) != 0u;
     delivered += d;
     active += d ? 1u : 0u;
     return d;
@@ -653,14 +894,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     uint32_t dz = 0;
     if(!T.reducible)
       for(uint32_t i = tid; i < nact; i += kZoneThreads)
-        if(s_cnt[i]) dz += drain_actor(T, tz, i);
+        if(s_cnt[i] || s_tb[i]) dz += drain_actor(T, tz, i);
     if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
   }
   else
   {
     for(uint32_t i = tid; i < nact; i += kZoneThreads)
     {
-      if(s_cnt[i] == 0) continue;
+      if(s_cnt[i] == 0 && s_tb[i] == 0) continue;
       const int t = type_of_local(L0 + i);
       if(t < 0 || c_types[t].reducible) continue;
       const uint32_t d = drain_actor(c_types[t], t, i);
@@ -671,6 +912,43 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   applied = a.applied;
   if(applied && a.applied_type >= 0)
     atomicAdd(&s_bytype[a.applied_type], (unsigned long long)applied);
+  // ---- 3b. carry-out: every actor's unhandled remainder, canonical, to the
+  //      next step's carry buffer (none in the usual step) -----------------------------
+  uint32_t ncout = 0;
+  if(__syncthreads_or(any_rem))
+  {
+    ncout = block_scan_zone(s_aux, s_tmp);
+    for(uint32_t i = tid; i < nact; i += kZoneThreads)
+    {
+      const uint32_t co = s_aux[i];
+      const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
+      if(rem == 0) continue;
+      const uint32_t n = s_cnt[i];
+      if(use_idx)
+        carry_out(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
+      else
+        carry_out(AccS{Sz + s_off[i]}, n - rem, n, z, co, nxt);
+    }
+  }
+  if(tid == 0) c_eng.carry_n[nxt][z] = ncout;   // past cap: the tail is in the spill list
+  // trigger bytes for the next step (only where some are set, or were)
+  const uint32_t ntrig = s_ntrig;
+  if(ntrig || ztn)
+  {
+    if(R == 1)
+      for(uint32_t i = tid; i < kZone / 4; i += kZoneThreads)
+      {
+        if(4 * i < nact)
+          reinterpret_cast<uint32_t*>(tb_out + L0)[i] = reinterpret_cast<const uint32_t*>(s_tb)[i];
+      }
+    else
+      for(uint32_t i = tid; i < nact; i += kZoneThreads) tb_out[(L0 + i) * R + me] = s_tb[i];
+    if(tid == 0)
+    {
+      c_eng.ztrig[nxt][z] = ntrig;
+      if(ntrig) atomicAdd(&c_eng.trig_n[(sidx + 1u) % 3u], ntrig);
+    }
+  }
   __syncthreads();
   GPA_STAMP(4);
   if(tid < GPU_ACTOR_MAX_TYPES && s_bytype[tid])
