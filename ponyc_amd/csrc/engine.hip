@@ -30,7 +30,7 @@ using namespace gpa;
 
 // gups Updater tables (gups_basic/main.pony:145-155: table[k] = k + index*size),
 // one thread per word (field-major state[k * lcount + li]).
-__global__ void __launch_bounds__(kBlock) k_construct_table(uint32_t t, uint32_t n_live)
+__global__ void __launch_bounds__(kBlock) k_construct_table(uint32_t t, uint32_t live)
 {
   const TypeDev& T = c_types[t];
   const uint64_t n = T.lcount;
@@ -40,21 +40,24 @@ __global__ void __launch_bounds__(kBlock) k_construct_table(uint32_t t, uint32_t
       x += (uint64_t)gridDim.x * kBlock)
   {
     const uint64_t k = x / n, li = x - k * n;
-    if(li >= n_live) continue;
     const uint64_t L = T.lfirst + li;
     const uint64_t i = L * c_eng.nranks + c_eng.rank - T.first;
+    if(i >= live) continue;
     T.state[x] = k + i * size;
   }
 }
 
-// pony_create's constructor run: initial state of a freshly created type.
-__global__ void __launch_bounds__(kBlock) k_construct(uint32_t t, uint32_t n_live)
+// pony_create's constructor run: initial state of a freshly created type;
+// the first `live` ids of the type (the rest are reserved for actors its
+// behaviours create, and stay zeroed until then).
+__global__ void __launch_bounds__(kBlock) k_construct(uint32_t t, uint32_t live)
 {
   const TypeDev& T = c_types[t];
   const uint32_t li = blockIdx.x * kBlock + threadIdx.x;
-  if(li >= n_live) return;      // reserved (not yet spawned) actors stay zeroed
+  if(li >= T.lcount) return;
   const uint32_t L = T.lfirst + li;
   const uint64_t i = (uint64_t)L * c_eng.nranks + c_eng.rank - T.first;   // index in type
+  if(i >= live) return;
   const size_t n = T.lcount;
   uint64_t* st = T.state;
   switch(T.ht)
@@ -141,14 +144,15 @@ __global__ void __launch_bounds__(kLandThreads) k_spawn_land(const uint64_t* key
       const uint64_t slot = live[t] + (i - tstart[t]);
       if(slot < T.count)
       {
-        r[u].valid = true;
+        // every rank numbers the same gathered list; it lands its own actors
+        r[u].valid = c_eng.nranks == 1 || (T.first + slot) % c_eng.nranks == c_eng.rank;
         r[u].to = T.first + (uint32_t)slot;
         r[u].w = (uint32_t)(((k >> 4) & 0xFFFFull) << 16) | (uint32_t)((k & 0xFu) << 12);
         r[u].from = (uint32_t)(k >> 20);
         r[u].arg = arg[i];
       }
-      else
-        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+      else if(c_eng.rank == 0)
+        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);     // reserve exhausted
     }
   }
   land_records(r, cur, s_hist, s_base);
@@ -249,10 +253,13 @@ struct Engine {
   ncclComm_t comm = nullptr;
   XRec* d_xout = nullptr;
   XRec* d_xin = nullptr;
-  unsigned long long* d_xcount = nullptr;
-  unsigned long long* d_xrecv = nullptr;
+  unsigned long long* d_xc = nullptr;      // [2R + 2]: send counts, receive counts, scratch
+  unsigned long long* d_xcount = nullptr;  // d_xc
+  unsigned long long* d_xrecv = nullptr;   // d_xc + R
+  unsigned long long* h_xc = nullptr;      // pinned mirror of d_xc
+  unsigned int* d_spill_flag = nullptr;    // spill lists in use on any rank (summed)
   uint32_t xcap = 0;
-  std::vector<unsigned long long> h_xcount, h_xrecv;
+  std::vector<unsigned long long> h_xcount, h_xrecv;   // host transport
   uint64_t remote_total = 0;
   // host transport (gpu_actor_set_transport)
   gpu_actor_alltoallv_fn xp_a2a = nullptr;
@@ -383,6 +390,7 @@ int upload_types()
     e.ztrig[p] = g.d_ztrig[p];
   }
   e.muted_on = g.d_muted_on;
+  e.spill_flag = g.d_spill_flag;
   e.trig_n = g.d_trig_n;
   e.spill[0] = g.d_spill[0]; e.spill[1] = g.d_spill[1];
   e.spill_n = g.d_sstat ? g.d_sstat->spill_n : nullptr;
@@ -476,6 +484,7 @@ int fixup_spill()
     HIPCK(hipGetLastError());
   }
   HIPCK(hipMemsetAsync(g.d_sstat, 0, sizeof(Engine::SpillStat), g.stream));
+  HIPCK(hipMemsetAsync(g.d_spill_flag, 0, sizeof(unsigned int), g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   g.fixups++;
@@ -616,75 +625,90 @@ int check_sticky()
   return g.sticky;
 }
 
-// Cross-rank exchange of the records a step produced for other ranks:
-// counts all-to-all, then grouped point-to-point transfers (RCCL over xGMI),
-// then k_xinject lands them for the next step. Two small D2H count reads.
-// Host transport: the same exchange with records staged through pinned host
-// memory and the collectives done by the registered callbacks (gloo etc.).
-int exchange_host(uint64_t& total)
+// Cross-rank exchange after a step (n_ranks > 1), with ONE synchronisation:
+//   device: counts all-to-all, trigger count summed (RCCL), then one pinned
+//   readback of send counts, receive counts, the trigger count and the spill
+//   status; host: grouped ncclSend/ncclRecv of the records over xGMI; device:
+//   k_xinject lands them; the trigger bytes are merged when any actor
+//   triggers muting (or did last time on this parity); a spill flag summed
+//   over ranks (k_spill_flag + allreduce, no readback) lets every rank's next
+//   k_step halt alike when any zone overflowed.
+// The host transport (gpu_actor_set_transport) does the same through its
+// callbacks, with the records staged through pinned host memory.
+__global__ void k_spill_flag(unsigned int* flag)
 {
-  const uint32_t n = R();
-  HIPCK(hipMemcpyAsync(g.h_xcount.data(), g.d_xcount, n * sizeof(unsigned long long),
-    hipMemcpyDeviceToHost, g.stream));
-  HIPCK(hipStreamSynchronize(g.stream));
-  std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n);
-  for(uint32_t p = 0; p < n; ++p)
-    sc[p] = p == rank() ? 0 : std::min<unsigned long long>(g.h_xcount[p], g.xcap);
-  std::vector<uint64_t> rc(n, 0);
-  if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rc.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
-  uint64_t soff = 0, roff = 0;
-  for(uint32_t p = 0; p < n; ++p)
-  {
-    rc[p] = std::min<uint64_t>(rc[p], g.xcap);
-    if(sc[p])
-      HIPCK(hipMemcpyAsync(g.h_xout + soff, g.d_xout + (size_t)p * g.xcap, sc[p] * sizeof(XRec),
-        hipMemcpyDeviceToHost, g.stream));
-    soff += sc[p];
-    roff += rc[p];
-    sb[p] = sc[p] * sizeof(XRec);
-    rb[p] = rc[p] * sizeof(XRec);
-  }
-  HIPCK(hipStreamSynchronize(g.stream));
-  if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
-  if(roff)
-    HIPCK(hipMemcpyAsync(g.d_xin, g.h_xin, roff * sizeof(XRec), hipMemcpyHostToDevice, g.stream));
-  // per-peer counts for k_xinject (the sender's rank of each record)
-  for(uint32_t p = 0; p < n; ++p) g.h_xrecv[p] = rc[p];
-  HIPCK(hipMemcpyAsync(g.d_xrecv, g.h_xrecv.data(), n * sizeof(unsigned long long),
-    hipMemcpyHostToDevice, g.stream));
-  total = roff;
-  return 0;
+  *flag = c_eng.spill_n[0] + c_eng.spill_n[1];
 }
 
-int exchange(uint32_t land_par)
+int exchange_step(uint32_t step_sidx)
 {
-  const uint32_t n = R();
-  uint64_t off = 0;
+  const uint32_t n = R(), land_par = g.par, tslot = (step_sidx + 1) % 3;
+  unsigned int tcount = 0;
+  uint64_t total = 0;
   if(g.xp_a2a)
   {
-    int rc = exchange_host(off);
-    if(rc) return rc;
+    unsigned int tloc = 0;
+    HIPCK(hipMemcpyAsync(g.h_xc, g.d_xcount, n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+      g.stream));
+    HIPCK(hipMemcpyAsync(&tloc, g.d_trig_n + tslot, sizeof(tloc), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+      g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n), rc(n, 0);
+    for(uint32_t p = 0; p < n; ++p)
+      sc[p] = p == rank() ? 0 : std::min<unsigned long long>(g.h_xc[p], g.xcap);
+    if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rc.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
+    uint64_t t64 = tloc;
+    if(g.xp_ar(g.xp_ctx, &t64, 1) != 0) return GPU_ACTOR_ECOMM;
+    tcount = (unsigned int)t64;
+    HIPCK(hipMemcpyAsync(g.d_trig_n + tslot, &tcount, sizeof(tcount), hipMemcpyHostToDevice,
+      g.stream));
+    uint64_t soff = 0;
+    for(uint32_t p = 0; p < n; ++p)
+    {
+      rc[p] = std::min<uint64_t>(rc[p], g.xcap);
+      if(sc[p])
+        HIPCK(hipMemcpyAsync(g.h_xout + soff, g.d_xout + (size_t)p * g.xcap, sc[p] * sizeof(XRec),
+          hipMemcpyDeviceToHost, g.stream));
+      soff += sc[p];
+      total += rc[p];
+      sb[p] = sc[p] * sizeof(XRec);
+      rb[p] = rc[p] * sizeof(XRec);
+      g.h_xc[n + p] = rc[p];
+    }
+    HIPCK(hipStreamSynchronize(g.stream));
+    if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
+    if(total)
+      HIPCK(hipMemcpyAsync(g.d_xin, g.h_xin, total * sizeof(XRec), hipMemcpyHostToDevice, g.stream));
+    // per-peer counts for k_xinject (the sender's rank of each record)
+    HIPCK(hipMemcpyAsync(g.d_xrecv, g.h_xc + n, n * sizeof(unsigned long long),
+      hipMemcpyHostToDevice, g.stream));
   }
   else
   {
-    HIPCK(hipMemcpyAsync(g.h_xcount.data(), g.d_xcount, n * sizeof(unsigned long long),
-      hipMemcpyDeviceToHost, g.stream));
     NCCLCK(ncclAllToAll(g.d_xcount, g.d_xrecv, 1, ncclUint64, g.comm, g.stream));
-    HIPCK(hipMemcpyAsync(g.h_xrecv.data(), g.d_xrecv, n * sizeof(unsigned long long),
+    NCCLCK(ncclAllReduce(g.d_trig_n + tslot, g.d_trig_n + tslot, 1, ncclUint32, ncclSum, g.comm,
+      g.stream));
+    HIPCK(hipMemcpyAsync(g.h_xc, g.d_xc, 2 * n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+      g.stream));
+    HIPCK(hipMemcpyAsync(g.h_xc + 2 * n, g.d_trig_n + tslot, sizeof(unsigned int),
       hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
+    HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+      g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));            // the step's one synchronisation
+    tcount = (unsigned int)(g.h_xc[2 * n] & 0xFFFFFFFFull);
     std::vector<uint64_t> roff(n);
     for(uint32_t p = 0; p < n; ++p)
     {
-      roff[p] = off;
-      off += std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
+      roff[p] = total;
+      total += std::min<unsigned long long>(g.h_xc[n + p], g.xcap);
     }
     NCCLCK(ncclGroupStart());
     for(uint32_t p = 0; p < n; ++p)
     {
       if(p == rank()) continue;
-      const uint64_t sc = std::min<unsigned long long>(g.h_xcount[p], g.xcap);
-      const uint64_t rc = std::min<unsigned long long>(g.h_xrecv[p], g.xcap);
+      const uint64_t sc = std::min<unsigned long long>(g.h_xc[p], g.xcap);
+      const uint64_t rc = std::min<unsigned long long>(g.h_xc[n + p], g.xcap);
       if(sc) NCCLCK(ncclSend(g.d_xout + (size_t)p * g.xcap, sc * sizeof(XRec), ncclUint8, p,
         g.comm, g.stream));
       if(rc) NCCLCK(ncclRecv(g.d_xin + roff[p], rc * sizeof(XRec), ncclUint8, p, g.comm,
@@ -692,7 +716,6 @@ int exchange(uint32_t land_par)
     }
     NCCLCK(ncclGroupEnd());
   }
-  const uint64_t total = off;
   g.remote_total += total;
   if(total)
   {
@@ -701,6 +724,41 @@ int exchange(uint32_t land_par)
     HIPCK(hipGetLastError());
   }
   HIPCK(hipMemsetAsync(g.d_xcount, 0, n * sizeof(unsigned long long), g.stream));
+  // trigger bytes of parity land_par: every rank's own bytes summed (each
+  // byte has one writer, so the sum is the merge)
+  if(tcount || g.trig_stale[land_par])
+  {
+    if(g.xp_ar)
+    {
+      std::vector<uint64_t> h(g.trig_bytes / 8);
+      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[land_par], g.trig_bytes, hipMemcpyDeviceToHost,
+        g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+      if(g.xp_ar(g.xp_ctx, h.data(), h.size()) != 0) return GPU_ACTOR_ECOMM;
+      HIPCK(hipMemcpyAsync(g.d_trig[land_par], h.data(), g.trig_bytes, hipMemcpyHostToDevice,
+        g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+    }
+    else
+      NCCLCK(ncclAllReduce(g.d_trig_own[land_par], g.d_trig[land_par], g.trig_bytes, ncclUint8,
+        ncclSum, g.comm, g.stream));
+  }
+  g.trig_stale[land_par] = tcount != 0;
+  // did any rank's zone overflow (this step or its landing)? summed on device
+  hipLaunchKernelGGL(k_spill_flag, dim3(1), dim3(1), 0, g.stream, g.d_spill_flag);
+  HIPCK(hipGetLastError());
+  if(g.xp_ar)
+  {
+    unsigned int f = 0;
+    HIPCK(hipMemcpyAsync(&f, g.d_spill_flag, sizeof(f), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    uint64_t f64 = f;
+    if(g.xp_ar(g.xp_ctx, &f64, 1) != 0) return GPU_ACTOR_ECOMM;
+    f = (unsigned int)std::min<uint64_t>(f64, 0xFFFFFFFFull);
+    HIPCK(hipMemcpyAsync(g.d_spill_flag, &f, sizeof(f), hipMemcpyHostToDevice, g.stream));
+  }
+  else
+    NCCLCK(ncclAllReduce(g.d_spill_flag, g.d_spill_flag, 1, ncclUint32, ncclSum, g.comm, g.stream));
   return 0;
 }
 
@@ -732,77 +790,146 @@ step_kernel_t pick_step_kernel()
 // Ids and landing for the actors the last step's behaviours created: the
 // records are sorted by (type, creator, seq) — the canonical order — and
 // numbered after each type's live actors (k_spawn_*). One small readback per
-// step, only for engines with a reserve.
+// step, only for engines with a reserve. With n_ranks > 1 every rank gathers
+// every rank's records (count allgather, then grouped send/recv, or the host
+// transport), sorts the same list, numbers alike, and lands the constructor
+// messages of the actors it owns (owner = id % n_ranks): the ids equal a
+// single rank's (pony_create inside behaviours is rank-agnostic,
+// actor.c:688-734).
 int spawn_process(uint32_t cur)
 {
   unsigned int n = 0;
   HIPCK(hipMemcpyAsync(&n, g.d_spawn_n, sizeof(n), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
-  if(n == 0) return 0;
   n = std::min(n, g.spawn_cap);
+  uint64_t* key = g.d_skey[0];
+  uint64_t* arg = g.d_sarg[0];
+  uint32_t total = n;
+  if(R() > 1)
+  {
+    const uint32_t nr = R();
+    std::vector<uint64_t> cnt(nr, 0);
+    if(g.xp_a2a)
+    {
+      std::vector<uint64_t> mine(nr, n), b8(nr, sizeof(uint64_t));
+      if(g.xp_a2a(g.xp_ctx, mine.data(), b8.data(), cnt.data(), b8.data()) != 0)
+        return GPU_ACTOR_ECOMM;
+    }
+    else
+    {
+      unsigned long long* dc = g.d_xc + 2 * nr;     // scratch words of the counts block
+      const unsigned long long mine = n;
+      HIPCK(hipMemcpyAsync(dc, &mine, sizeof(mine), hipMemcpyHostToDevice, g.stream));
+      unsigned long long* dall = nullptr;
+      HIPCK(hipMalloc(&dall, nr * sizeof(unsigned long long)));
+      NCCLCK(ncclAllGather(dc, dall, 1, ncclUint64, g.comm, g.stream));
+      HIPCK(hipMemcpyAsync(cnt.data(), dall, nr * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
+      HIPCK(hipStreamSynchronize(g.stream));
+      HIPCK(hipFree(dall));
+    }
+    // rank order, clipped to the reserve (the same clip on every rank)
+    std::vector<uint64_t> off(nr);
+    uint64_t acc = 0;
+    for(uint32_t p = 0; p < nr; ++p)
+    {
+      cnt[p] = std::min<uint64_t>(cnt[p], g.spawn_cap - acc);
+      off[p] = acc;
+      acc += cnt[p];
+    }
+    total = (uint32_t)acc;
+    if(total == 0) return 0;
+    n = (uint32_t)cnt[rank()];
+    // gathered into [1], local records first copied to their own slot
+    if(n)
+    {
+      HIPCK(hipMemcpyAsync(g.d_skey[1] + off[rank()], g.d_skey[0], n * sizeof(uint64_t),
+        hipMemcpyDeviceToDevice, g.stream));
+      HIPCK(hipMemcpyAsync(g.d_sarg[1] + off[rank()], g.d_sarg[0], n * sizeof(uint64_t),
+        hipMemcpyDeviceToDevice, g.stream));
+    }
+    if(g.xp_a2a)
+    {
+      std::vector<uint64_t> hk(total), ha(total), sb(nr), rb(nr);
+      std::vector<uint64_t> lk(n), la(n);
+      if(n)
+      {
+        HIPCK(hipMemcpyAsync(lk.data(), g.d_skey[0], n * sizeof(uint64_t), hipMemcpyDeviceToHost,
+          g.stream));
+        HIPCK(hipMemcpyAsync(la.data(), g.d_sarg[0], n * sizeof(uint64_t), hipMemcpyDeviceToHost,
+          g.stream));
+      }
+      HIPCK(hipStreamSynchronize(g.stream));
+      // every peer gets our n records; we get each peer's
+      std::vector<uint64_t> sendk, senda;
+      for(uint32_t p = 0; p < nr; ++p)
+      {
+        sb[p] = (p == rank() ? 0 : n) * sizeof(uint64_t);
+        rb[p] = (p == rank() ? 0 : cnt[p]) * sizeof(uint64_t);
+        if(p != rank()) { sendk.insert(sendk.end(), lk.begin(), lk.end()); senda.insert(senda.end(), la.begin(), la.end()); }
+      }
+      std::vector<uint64_t> rk(total), ra(total);
+      if(g.xp_a2a(g.xp_ctx, sendk.data(), sb.data(), rk.data(), rb.data()) != 0) return GPU_ACTOR_ECOMM;
+      if(g.xp_a2a(g.xp_ctx, senda.data(), sb.data(), ra.data(), rb.data()) != 0) return GPU_ACTOR_ECOMM;
+      uint64_t at = 0;
+      for(uint32_t p = 0; p < nr; ++p)
+      {
+        if(p == rank() || !cnt[p]) continue;
+        HIPCK(hipMemcpyAsync(g.d_skey[1] + off[p], rk.data() + at, cnt[p] * sizeof(uint64_t),
+          hipMemcpyHostToDevice, g.stream));
+        HIPCK(hipMemcpyAsync(g.d_sarg[1] + off[p], ra.data() + at, cnt[p] * sizeof(uint64_t),
+          hipMemcpyHostToDevice, g.stream));
+        at += cnt[p];
+      }
+      HIPCK(hipStreamSynchronize(g.stream));
+    }
+    else
+    {
+      NCCLCK(ncclGroupStart());
+      for(uint32_t p = 0; p < nr; ++p)
+      {
+        if(p == rank()) continue;
+        if(n)
+        {
+          NCCLCK(ncclSend(g.d_skey[0], n, ncclUint64, p, g.comm, g.stream));
+          NCCLCK(ncclSend(g.d_sarg[0], n, ncclUint64, p, g.comm, g.stream));
+        }
+        if(cnt[p])
+        {
+          NCCLCK(ncclRecv(g.d_skey[1] + off[p], cnt[p], ncclUint64, p, g.comm, g.stream));
+          NCCLCK(ncclRecv(g.d_sarg[1] + off[p], cnt[p], ncclUint64, p, g.comm, g.stream));
+        }
+      }
+      NCCLCK(ncclGroupEnd());
+    }
+    // sort input: the gathered list
+    HIPCK(hipMemcpyAsync(g.d_skey[0], g.d_skey[1], total * sizeof(uint64_t),
+      hipMemcpyDeviceToDevice, g.stream));
+    HIPCK(hipMemcpyAsync(g.d_sarg[0], g.d_sarg[1], total * sizeof(uint64_t),
+      hipMemcpyDeviceToDevice, g.stream));
+  }
+  if(total == 0) return 0;
   size_t need = 0;
-  HIPCK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, g.d_skey[0], g.d_skey[1], g.d_sarg[0],
-    g.d_sarg[1], (int)n, 0, 56, g.stream));
+  HIPCK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, key, g.d_skey[1], arg,
+    g.d_sarg[1], (int)total, 0, 56, g.stream));
   if(need > g.sort_tmp_bytes)
   {
     if(g.d_sort_tmp) HIPCK(hipFree(g.d_sort_tmp));
     HIPCK(hipMalloc(&g.d_sort_tmp, need));
     g.sort_tmp_bytes = need;
   }
-  HIPCK(hipcub::DeviceRadixSort::SortPairs(g.d_sort_tmp, need, g.d_skey[0], g.d_skey[1],
-    g.d_sarg[0], g.d_sarg[1], (int)n, 0, 56, g.stream));
+  HIPCK(hipcub::DeviceRadixSort::SortPairs(g.d_sort_tmp, need, key, g.d_skey[1],
+    arg, g.d_sarg[1], (int)total, 0, 56, g.stream));
   HIPCK(hipMemsetAsync(g.d_tstart, 0xFF, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t), g.stream));
   HIPCK(hipMemsetAsync(g.d_tcnt, 0, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t), g.stream));
-  hipLaunchKernelGGL(k_spawn_scan, dim3(blocks_for(n)), dim3(kBlock), 0, g.stream,
-    (const uint64_t*)g.d_skey[1], n, g.d_tstart, g.d_tcnt);
-  hipLaunchKernelGGL(k_spawn_land, dim3(blocks_for(n, kLandRecs)), dim3(kLandThreads), 0, g.stream,
-    (const uint64_t*)g.d_skey[1], (const uint64_t*)g.d_sarg[1], n, (const uint32_t*)g.d_tstart,
-    (const unsigned long long*)g.d_live, cur);
+  hipLaunchKernelGGL(k_spawn_scan, dim3(blocks_for(total)), dim3(kBlock), 0, g.stream,
+    (const uint64_t*)g.d_skey[1], total, g.d_tstart, g.d_tcnt);
+  hipLaunchKernelGGL(k_spawn_land, dim3(blocks_for(total, kLandRecs)), dim3(kLandThreads), 0,
+    g.stream, (const uint64_t*)g.d_skey[1], (const uint64_t*)g.d_sarg[1], total,
+    (const uint32_t*)g.d_tstart, (const unsigned long long*)g.d_live, cur);
   hipLaunchKernelGGL(k_spawn_commit, dim3(1), dim3(64), 0, g.stream,
     (const uint32_t*)g.d_tcnt, g.d_live);
   HIPCK(hipGetLastError());
   HIPCK(hipMemsetAsync(g.d_spawn_n, 0, sizeof(unsigned int), g.stream));
-  return 0;
-}
-
-// n_ranks > 1: the count of actors that trigger muting after step `sidx`
-// (summed over ranks in place), and, when any do (or the merged bytes of this
-// parity were nonzero last time), every rank's own trigger bytes summed into
-// the global array the next step reads (each byte has one writer, so the sum
-// is the merge).
-int merge_triggers(uint32_t sidx)
-{
-  const uint32_t slot = (sidx + 1) % 3, p = g.par;
-  unsigned int cnt = 0;
-  if(g.xp_ar)
-  {
-    HIPCK(hipMemcpyAsync(&cnt, g.d_trig_n + slot, sizeof(cnt), hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
-    uint64_t c64 = cnt;
-    if(g.xp_ar(g.xp_ctx, &c64, 1) != 0) return GPU_ACTOR_ECOMM;
-    cnt = (unsigned int)c64;
-    HIPCK(hipMemcpyAsync(g.d_trig_n + slot, &cnt, sizeof(cnt), hipMemcpyHostToDevice, g.stream));
-    if(cnt || g.trig_stale[p])
-    {
-      std::vector<uint64_t> h(g.trig_bytes / 8);
-      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[p], g.trig_bytes, hipMemcpyDeviceToHost, g.stream));
-      HIPCK(hipStreamSynchronize(g.stream));
-      if(g.xp_ar(g.xp_ctx, h.data(), h.size()) != 0) return GPU_ACTOR_ECOMM;
-      HIPCK(hipMemcpyAsync(g.d_trig[p], h.data(), g.trig_bytes, hipMemcpyHostToDevice, g.stream));
-      HIPCK(hipStreamSynchronize(g.stream));
-    }
-  }
-  else
-  {
-    NCCLCK(ncclAllReduce(g.d_trig_n + slot, g.d_trig_n + slot, 1, ncclUint32, ncclSum, g.comm,
-      g.stream));
-    HIPCK(hipMemcpyAsync(&cnt, g.d_trig_n + slot, sizeof(cnt), hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
-    if(cnt || g.trig_stale[p])
-      NCCLCK(ncclAllReduce(g.d_trig_own[p], g.d_trig[p], g.trig_bytes, ncclUint8, ncclSum, g.comm,
-        g.stream));
-  }
-  g.trig_stale[p] = cnt != 0;
   return 0;
 }
 
@@ -829,18 +956,18 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   g.sidx++;
   if(R() > 1)
   {
-    int rc = exchange(g.par);
+    int rc = exchange_step(step_sidx);
     if(rc) return rc;
-    rc = merge_triggers(step_sidx);
-    if(rc) return rc;
-    // steps never halt on the device with n_ranks > 1 (ranks would part
-    // ways): a zone that overflowed is grown before the next step
-    rc = read_sstat();
-    if(rc) return rc;
-    if(spill_pending())
+    if(g.h_sstat->halt)
     {
+      // this step did not run on any rank (a zone overflowed on some rank the
+      // step before): grow, then run it again from the same parity and index
       rc = fixup_spill();
       if(rc) return rc;
+      g.par ^= 1u;
+      g.sidx--;
+      HIPCK(hipMemsetAsync(g.d_pend + slot, 0, sizeof(unsigned long long), g.stream));
+      return launch_step(slot, e0, e1);
     }
   }
   if(g.spawn_cap)
@@ -934,8 +1061,9 @@ void free_all()
   if(g.d_msgs) (void)hipFree(g.d_msgs);
   if(g.d_xout) (void)hipFree(g.d_xout);
   if(g.d_xin) (void)hipFree(g.d_xin);
-  if(g.d_xcount) (void)hipFree(g.d_xcount);
-  if(g.d_xrecv) (void)hipFree(g.d_xrecv);
+  if(g.d_xc) (void)hipFree(g.d_xc);
+  if(g.h_xc) (void)hipHostFree(g.h_xc);
+  if(g.d_spill_flag) (void)hipFree(g.d_spill_flag);
   if(g.h_xout) (void)hipHostFree(g.h_xout);
   if(g.h_xin) (void)hipHostFree(g.h_xin);
   for(hipEvent_t e : g.ev) (void)hipEventDestroy(e);
@@ -1079,6 +1207,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
       HIPCK(hipMemsetAsync(g.d_trig_own[p], 0, g.trig_bytes, g.stream));
     }
   }
+  HIPCK(hipMalloc(&g.d_spill_flag, sizeof(unsigned int)));
+  HIPCK(hipMemsetAsync(g.d_spill_flag, 0, sizeof(unsigned int), g.stream));
   HIPCK(hipMalloc(&g.d_trig_n, 4 * sizeof(unsigned int)));
   HIPCK(hipMemsetAsync(g.d_trig_n, 0, 4 * sizeof(unsigned int), g.stream));
   HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
@@ -1104,9 +1234,11 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
     }
     HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
     HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
-    HIPCK(hipMalloc(&g.d_xcount, R() * sizeof(unsigned long long)));
-    HIPCK(hipMalloc(&g.d_xrecv, R() * sizeof(unsigned long long)));
-    HIPCK(hipMemsetAsync(g.d_xcount, 0, R() * sizeof(unsigned long long), g.stream));
+    HIPCK(hipMalloc(&g.d_xc, (2 * R() + 2) * sizeof(unsigned long long)));
+    HIPCK(hipMemsetAsync(g.d_xc, 0, (2 * R() + 2) * sizeof(unsigned long long), g.stream));
+    HIPCK(hipHostMalloc(&g.h_xc, (2 * R() + 2) * sizeof(unsigned long long), hipHostMallocDefault));
+    g.d_xcount = g.d_xc;
+    g.d_xrecv = g.d_xc + R();
     g.h_xcount.assign(R(), 0);
     g.h_xrecv.assign(R(), 0);
   }
@@ -1171,6 +1303,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
   g.deferred.clear();
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
+  g.d_xc = nullptr; g.h_xc = nullptr; g.d_spill_flag = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
   g.h_xout = g.h_xin = nullptr;
   return 0;
@@ -1236,7 +1369,6 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   if(type_id >= GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
   HostType& t = g.types[type_id];
   if(!t.registered || t.created || count == 0) return GPU_ACTOR_EINVAL;
-  if(t.reserve && R() > 1) return GPU_ACTOR_EINVAL;
   const uint64_t live = count;
   count += t.reserve;                    // ids for the type's spawned actors
   if(g.n_actors + count > g.cfg.max_actors) return GPU_ACTOR_ERANGE;
@@ -1264,11 +1396,11 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   if(rc) return rc;
   rc = upload_types();
   if(rc) return rc;
-  hipLaunchKernelGGL(k_construct, dim3(blocks_for(live)), dim3(kBlock), 0, g.stream,
-    type_id, (uint32_t)std::min<uint64_t>(live, t.lcount));
+  hipLaunchKernelGGL(k_construct, dim3(blocks_for(std::max<uint64_t>(t.lcount, 1))), dim3(kBlock), 0,
+    g.stream, type_id, (uint32_t)live);
   if(t.ht == GPU_ACTOR_HT_GUPS_UPDATER)
     hipLaunchKernelGGL(k_construct_table, dim3(4096), dim3(kBlock), 0, g.stream,
-      type_id, (uint32_t)std::min<uint64_t>(live, t.lcount));
+      type_id, (uint32_t)live);
   HIPCK(hipGetLastError());
   const unsigned long long live_ull = live;
   HIPCK(hipMemcpyAsync(g.d_live + type_id, &live_ull, sizeof(live_ull), hipMemcpyHostToDevice,
@@ -1301,7 +1433,6 @@ GPU_ACTOR_API int gpu_actor_type_reserve(uint32_t type_id, uint64_t n)
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(type_id >= GPU_ACTOR_MAX_TYPES || !g.types[type_id].registered ||
     g.types[type_id].created) return GPU_ACTOR_EINVAL;
-  if(n && R() > 1) return GPU_ACTOR_EINVAL;
   if(n > g.cfg.max_actors) return GPU_ACTOR_ERANGE;
   g.types[type_id].reserve = n;
   return 0;

@@ -145,6 +145,7 @@ struct EngDev {
   uint8_t* trig[2];
   uint8_t* trig_own[2];
   uint32_t* muted_on;
+  unsigned int* spill_flag;      // n_ranks > 1: spill lists in use on any rank
   uint32_t* ztrig[2];
   unsigned int* trig_n;           // [3]
   SpillRec* spill[2];

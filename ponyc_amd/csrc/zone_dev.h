@@ -408,15 +408,15 @@ __device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, ui
 constexpr uint32_t kBigGroup = 128;
 constexpr uint32_t kMaxBig = 32;            // big groups sorted per round of the loop
 constexpr uint32_t kPayBits = 20;           // payload bits of an item (group <= 2^20)
-constexpr uint32_t kSortWork = 256 + kZoneWaves * 256;   // u32 of LDS the sort borrows
+constexpr uint32_t kSortWork = 512 + kZoneWaves * 256;   // u32 of LDS the sort borrows
 
 // Stable sort of n items in a by item bits [lo, hi); b is scratch of n items.
 // The result ends in a. All threads call; ends behind a barrier.
 __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t hi,
   uint32_t* s_work)
 {
-  uint32_t* s_bin = s_work;                // [256] running base of each digit
-  uint32_t* s_wc = s_work + 256;           // [kZoneWaves][256] this tile's counts per wave
+  uint32_t* s_bin = s_work;                // [2][256] running base of each digit (double-buffered)
+  uint32_t* s_wc = s_work + 512;           // [kZoneWaves][256] this tile's counts per wave
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t* src = a;
@@ -436,7 +436,7 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
 #pragma unroll
       for(int k = 0; k < 4; ++k) { s_bin[lane * 4 + k] = run; run += v[k]; }
     }
-    __syncthreads();
+    uint32_t cb = 0;                       // which half of s_bin holds this tile's bases
     for(uint32_t t0 = 0; t0 < n; t0 += kZoneThreads)
     {
       const uint32_t i = t0 + tid;
@@ -455,21 +455,21 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
       __builtin_amdgcn_wave_barrier();
       const uint32_t rank = __popcll(same & lt);
       if(valid && rank == 0) s_wc[wv * 256 + d] = __popcll(same);
-      __syncthreads();
+      __syncthreads();                     // counts (and, first time, the bases) visible
       if(valid)
       {
-        uint32_t pre = s_bin[d];
+        uint32_t pre = s_bin[cb * 256 + d];
         for(uint32_t w = 0; w < wv; ++w) pre += s_wc[w * 256 + d];
         dst[pre + rank] = x;
       }
-      __syncthreads();
       for(uint32_t k = tid; k < 256; k += kZoneThreads)
       {
-        uint32_t c = 0;
+        uint32_t c = s_bin[cb * 256 + k];
         for(uint32_t w = 0; w < (uint32_t)kZoneWaves; ++w) c += s_wc[w * 256 + k];
-        s_bin[k] += c;
+        s_bin[(cb ^ 1u) * 256 + k] = c;
       }
-      __syncthreads();
+      cb ^= 1u;
+      __syncthreads();                     // every read of s_wc and the old bases done
     }
     uint64_t* t = src; src = dst; dst = t;
   }
@@ -575,6 +575,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_ntrig;
   __shared__ uint32_t s_bigbits[kZone / 32];   // groups the workgroup sorted this step
   __shared__ uint32_t s_red3[3];
+  __shared__ uint32_t s_big[kMaxBig];
+  __shared__ uint32_t s_nbig;
   constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
@@ -583,7 +585,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // zones and lands those records before another step runs; until then every
   // step is a no-op (spill_n[cur] is final for this launch; halt is set only
   // by skipped steps, so every zone of a launch decides alike).
-  if(c_eng.nranks == 1 && (c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u))
+  // With n_ranks > 1 the decision is the spill flag summed over ranks after
+  // the last exchange, so every rank halts the same steps.
+  const bool halt_now = c_eng.nranks == 1 ? (c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u)
+                                          : (*c_eng.spill_flag != 0u);
+  if(halt_now)
   {
     if(z == 0 && tid == 0)
     {
@@ -754,26 +760,23 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // (s_bigbits marks them for drain_zone). The sort borrows s_dyn, which the
   // behaviours' bucket counts use next, and the zone's outbox / S scratch.
   for(uint32_t k = tid; k < kZone / 32; k += kZoneThreads) s_bigbits[k] = 0;
+  if(tid == 0) s_nbig = 0;
+  __syncthreads();
+  for(uint32_t i = tid; i < nact; i += kZoneThreads)
+    if(s_cnt[i] - s_ccnt[i] > kBigGroup)
+    {
+      const uint32_t k = atomicAdd(&s_nbig, 1u);
+      if(k < kMaxBig) s_big[k] = i;
+    }
+  __syncthreads();
   {
-    int any_big = 0;
-    for(uint32_t i = tid; i < nact; i += kZoneThreads)
-      any_big |= (s_cnt[i] - s_ccnt[i]) > kBigGroup;
-    if(__syncthreads_or(any_big))
+    const uint32_t nbig = min(s_nbig, kMaxBig);     // past kMaxBig: the lane sorts (slow, exact)
+    if(nbig)
     {
       uint64_t* ia = reinterpret_cast<uint64_t*>(c_eng.O + c_eng.zoff[z]);
-      for(uint32_t i0 = 0; i0 < nact; )
+      for(uint32_t k = 0; k < nbig; ++k)
       {
-        // the next actor (in slot order) with a big group: found by scanning
-        if(tid == 0)
-        {
-          uint32_t i = i0;
-          while(i < nact && (s_cnt[i] - s_ccnt[i]) <= kBigGroup) ++i;
-          s_tmp[kZoneWaves] = i;
-        }
-        __syncthreads();
-        const uint32_t i = s_tmp[kZoneWaves];
-        __syncthreads();
-        if(i >= nact) break;
+        const uint32_t i = s_big[k];
         const uint32_t g = s_cnt[i] - s_ccnt[i];
         bool ok;
         if(use_idx)
@@ -783,7 +786,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           ok = coop_sort_group(AccS{Sz + s_off[i]}, nullptr, Sz + s_off[i], s_ccnt[i], g, ia,
                                ia + g, Sz + 2 * cap, s_dyn, s_red3);
         if(ok && tid == 0) s_bigbits[i >> 5] |= 1u << (i & 31);
-        i0 = i + 1;
       }
       for(uint32_t b = tid; b < max(nb, kSortWork); b += kZoneThreads) s_dyn[b] = 0;
       __syncthreads();
@@ -918,16 +920,46 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   if(__syncthreads_or(any_rem))
   {
     ncout = block_scan_zone(s_aux, s_tmp);
+    if(tid == 0) s_nbig = 0;
+    __syncthreads();
     for(uint32_t i = tid; i < nact; i += kZoneThreads)
     {
       const uint32_t co = s_aux[i];
       const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
       if(rem == 0) continue;
+      if(rem > kBigGroup)
+      {
+        // a backlog (an overloaded receiver): copied by the whole workgroup
+        const uint32_t k = atomicAdd(&s_nbig, 1u);
+        if(k < kMaxBig) { s_big[k] = i; continue; }
+      }
       const uint32_t n = s_cnt[i];
       if(use_idx)
         carry_out(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
       else
         carry_out(AccS{Sz + s_off[i]}, n - rem, n, z, co, nxt);
+    }
+    __syncthreads();
+    const uint32_t nbig = min(s_nbig, kMaxBig);
+    for(uint32_t k = 0; k < nbig; ++k)
+    {
+      const uint32_t i = s_big[k];
+      const uint32_t co = s_aux[i];
+      const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
+      const uint32_t n = s_cnt[i];
+      ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
+      for(uint32_t j = tid; j < rem; j += kZoneThreads)
+      {
+        const ZRec r = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
+                               : AccS{Sz + s_off[i]}.rec(n - rem + j);
+        uint4 u;
+        u.x = r.w0; u.y = r.from; u.z = (uint32_t)r.arg; u.w = (uint32_t)(r.arg >> 32);
+        const uint32_t pos = co + j;
+        if(pos < cap)
+          *reinterpret_cast<uint4*>(cout + pos) = u;
+        else
+          spill_rec(nxt, kSpillCarry, z, pos, u);
+      }
     }
   }
   if(tid == 0) c_eng.carry_n[nxt][z] = ncout;   // past cap: the tail is in the spill list

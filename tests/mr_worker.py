@@ -31,6 +31,13 @@ CASES = {
     # 600 sends per source per step: sequence numbers past 511 use the high
     # bits of the 16-B cross-rank record's 14-bit seq (engine_dev.h XRec)
     "fifo_seq": (lambda e: W.fifo(e, 4, 3, 1, 600, mailbox_cap=2048), W.fifo_result, {}),
+    # actors created by behaviours: every rank numbers the gathered spawn list
+    "spreader": (lambda e: W.spreader(e, 10), W.spreader_result, {}),
+    # backpressure across ranks: overloaded sinks mute senders on the other rank
+    "mute": (lambda e: W.fifo(e, 600, 3, 3, 2, batch=10, mailbox_cap=16), W.fifo_result, {}),
+    # zone overflow on one rank halts the next step on every rank until grown
+    "spill": (lambda e: W.fifo(e, 300, 3, 4, 9, batch=4, mailbox_cap=1), W.fifo_result,
+              {"mailbox_cap": 1}),
 }
 
 
