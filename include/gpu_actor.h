@@ -287,7 +287,9 @@ GPU_ACTOR_API const char* gpu_actor_strerror(int code);
  *            BURST(m): m x PUSH(i << 32 | ++seq); if --bursts: BURST(m) to self
  *   FIFO_SINK state: [0] h (FNV-1a fold of args, order-sensitive) [1] n
  *            [2] FIFO violations [3..10] last seq per source slot
- *            params: [0] n sinks
+ *            params: [0] n sinks [1] yield period k (0 = never): the sink
+ *            calls the yield rule (pony_yield analogue) after
+ *            every k-th message it has received
  *            PUSH(arg): slot = ((arg >> 32) / n_sinks) % 8                   */
 #define GPU_ACTOR_HT_FIFO_SRC        9
 #define GPU_ACTOR_FIFO_BURST         0

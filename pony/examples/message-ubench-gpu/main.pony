@@ -22,12 +22,15 @@ actor Main is GpuRunNotify
     _gpu.param(0, 3, 5489)                // seed
     let first = _gpu.create_actors(0, _n)
     _gpu.param(0, 1, first)
+    // SyncLeader.tell_all_to_go: 5 rounds of pings as one chain (one sendv)
+    let m = GpuMsgs((5 * _n).usize())
     var k: U64 = 0
-    while k < 5 do                        // SyncLeader.tell_all_to_go
+    while k < 5 do
       var i: U64 = 0
-      while i < _n do _gpu.send(first + i, 0, 42); i = i + 1 end
+      while i < _n do m.push(first + i, 0, 42); i = i + 1 end
       k = k + 1
     end
+    _gpu.sendv(m)
     _gpu.run_async(this)
 
   be gpu_run_done(rc: I32, steps: U64) =>

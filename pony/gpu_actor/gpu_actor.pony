@@ -26,7 +26,7 @@ use @gpu_actor_create[I32](type_id: U32, count: U64, first: Pointer[U64])
 use @gpu_actor_type_reserve[I32](type_id: U32, n: U64)
 use @gpu_actor_type_live[I32](type_id: U32, live: Pointer[U64])
 use @gpu_actor_alloc_msgs[I32](n: U64, buf: Pointer[Pointer[GpuMsg]])
-use @gpu_actor_sendv[I32](first: Pointer[GpuMsg] tag, n: U64)
+use @gpu_actor_sendv[I32](first: Pointer[U64] tag, n: U64)
 use @gpu_actor_send[I32](to: U64, behaviour: U32, arg: U64)
 use @gpu_actor_run[I32](max_steps: U64, steps_done: Pointer[U64])
 use @gpu_actor_run_fixed[I32](n: U64)
@@ -51,6 +51,8 @@ primitive HtFaninAnalyzer fun apply(): U32 => 5
 primitive HtGupsStreamer fun apply(): U32 => 6    // examples/gups_basic
 primitive HtGupsUpdater fun apply(): U32 => 7
 primitive HtStorm fun apply(): U32 => 8
+primitive HtFifoSrc fun apply(): U32 => 9         // examples/overload shape
+primitive HtFifoSink fun apply(): U32 => 10
 primitive HtSpreader fun apply(): U32 => 11       // examples/spreader
 
 struct GpuMsg
@@ -58,6 +60,26 @@ struct GpuMsg
   var to: U32 = 0
   var behaviour: U32 = 0
   var arg: U64 = 0
+
+class GpuMsgs
+  """
+  A chain of messages for one gpu_actor_sendv (pony_chain + pony_sendv,
+  actor.c:773-817, 923-927): gpu_msg_t records packed two U64 words each
+  (to | behaviour << 32 little-endian, then arg), so one FFI call hands the
+  whole chain over, in order.
+  """
+  let _words: Array[U64]
+
+  new create(capacity: USize = 0) =>
+    _words = Array[U64](capacity * 2)
+
+  fun ref push(to: U64, behaviour: U32, arg: U64) =>
+    _words.push((to and 0xFFFF_FFFF) or (behaviour.u64() << 32))
+    _words.push(arg)
+
+  fun size(): USize => _words.size() / 2
+
+  fun cpointer(): Pointer[U64] tag => _words.cpointer()
 
 struct GpuActorConfig
   """gpu_actor_config_t."""
@@ -151,8 +173,17 @@ class GpuActors
     end
     first
 
+  fun config(type_id: U32, batch: U32, mailbox_cap: U32 = 0): I32 =>
+    """The fork's _batch() hint (actor.c:410-416) and the zone sizing hint."""
+    @gpu_actor_type_config(type_id, batch, mailbox_cap)
+
   fun send(to: U64, behaviour: U32, arg: U64): I32 =>
+    """pony_sendi: staged on the host, injected by the next run (no sync)."""
     @gpu_actor_send(to, behaviour, arg)
+
+  fun sendv(msgs: GpuMsgs box): I32 =>
+    """pony_sendv of a chain: one H2D copy for all of it."""
+    @gpu_actor_sendv(msgs.cpointer(), msgs.size().u64())
 
   fun run(max_steps: U64 = 0): U64 =>
     var steps: U64 = 0
