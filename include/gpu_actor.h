@@ -43,7 +43,10 @@ extern "C" {
 #define GPU_ACTOR_EINVAL       -1   /* bad argument / unknown type / bad id   */
 #define GPU_ACTOR_ENOMEM       -2   /* device or host allocation failed        */
 #define GPU_ACTOR_ENODEV       -3   /* no usable GPU                           */
-#define GPU_ACTOR_EMAILBOX     -4   /* a mailbox overflowed; messages dropped  */
+#define GPU_ACTOR_EMAILBOX     -4   /* messages lost: the per-step overflow list
+                                       was exhausted, or behaviours spawned past
+                                       a type's reserve (zone buffers that fill
+                                       spill and grow; they never drop)        */
 #define GPU_ACTOR_EHIP         -5   /* HIP runtime error                       */
 #define GPU_ACTOR_ESTATE       -6   /* not initialised / already initialised   */
 #define GPU_ACTOR_ERANGE       -7   /* sequence or id space exhausted: more than
