@@ -152,8 +152,13 @@ int main()
   };
   timeit("coalesced copy (read + write)", [&] { hipLaunchKernelGGL(k_copy, dim3(NZ), dim3(THREADS), 0, 0, src, dst); });
   timeit("coalesced read", [&] { hipLaunchKernelGGL(k_read, dim3(NZ), dim3(THREADS), 0, 0, src, sink); });
-  for(uint32_t T : {PER, 4096u, 2048u, 1024u})
+  // xm = 1: destinations ordered XCD-major inside every tile (b' = (b % 8) * 64
+  // + b / 8), so the 64 receivers an XCD runs read one contiguous stretch of
+  // each tile and share its boundary lines in their own L2
+  for(int xm = 0; xm < 2; ++xm)
+  for(uint32_t T : {PER, 5120u, 4096u, 2560u, 2048u})
   {
+    auto perm = [&](uint32_t b) { return xm ? (b % 8) * (NZ / 8) + b / 8 : b; };
     const uint32_t ntile = (PER + T - 1) / T, nseg = NZ * ntile;
     // push: chunk of (source s, dest d) inside d's region, sources in a shuffled order
     std::vector<uint32_t> cnt((size_t)NZ * NZ, 0);
@@ -177,13 +182,13 @@ int main()
       {
         const uint32_t i0 = t * T, i1 = std::min(PER, i0 + T);
         std::vector<uint32_t> tc(NZ, 0), tpre(NZ + 1, 0), tcur(NZ, 0);
-        for(uint32_t i = i0; i < i1; ++i) tc[dstz[(size_t)s * PER + i]]++;
+        for(uint32_t i = i0; i < i1; ++i) tc[perm(dstz[(size_t)s * PER + i])]++;
         for(uint32_t b = 0; b < NZ; ++b) tpre[b + 1] = tpre[b] + tc[b];
         std::vector<std::pair<uint32_t, uint32_t>> ps;
         for(uint32_t i = i0; i < i1; ++i)
         {
-          const uint32_t b = dstz[(size_t)s * PER + i];
-          ps.push_back({tpre[b] + tcur[b]++, chunk[(size_t)s * NZ + b] + cur[b]++});
+          const uint32_t b = dstz[(size_t)s * PER + i], bp = perm(b);
+          ps.push_back({tpre[bp] + tcur[bp]++, chunk[(size_t)s * NZ + b] + cur[b]++});
         }
         // record at sorted slot k of the tile goes to push position / pull position
         std::sort(ps.begin(), ps.end());
@@ -195,8 +200,8 @@ int main()
         const uint32_t g = s * ntile + t;
         for(uint32_t b = 0; b < NZ; ++b)
         {
-          st[(size_t)b * nseg + g] = s * REGION + i0 + tpre[b];
-          cn[(size_t)b * nseg + g] = tc[b];
+          st[(size_t)b * nseg + g] = s * REGION + i0 + tpre[perm(b)];
+          cn[(size_t)b * nseg + g] = tc[perm(b)];
         }
       }
     }
@@ -209,10 +214,10 @@ int main()
     CK(hipMemcpy(dcn, cn.data(), (size_t)NZ * nseg * 4, hipMemcpyHostToDevice));
     char nm[96];
     snprintf(nm, sizeof nm, "push, tile %u (runs ~%.1f)", T, (double)T / NZ);
-    timeit(nm, [&] { hipLaunchKernelGGL(k_scatter, dim3(NZ), dim3(THREADS), 0, 0, src, dpush, dst); });
+    if(!xm) timeit(nm, [&] { hipLaunchKernelGGL(k_scatter, dim3(NZ), dim3(THREADS), 0, 0, src, dpush, dst); });
     if(nseg <= NZ * 8)
     {
-      snprintf(nm, sizeof nm, "pull read, tile %u (runs ~%.1f)", T, (double)T / NZ);
+      snprintf(nm, sizeof nm, "pull read%s, tile %u (runs ~%.1f)", xm ? " xcd-major" : "", T, (double)T / NZ);
       timeit(nm, [&] { hipLaunchKernelGGL(k_pull_read, dim3(NZ), dim3(THREADS), 0, 0, src, dst_, dcn, nseg, sink); });
     }
     CK(hipFree(dpush)); CK(hipFree(dst_)); CK(hipFree(dcn));
