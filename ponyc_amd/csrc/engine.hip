@@ -232,20 +232,8 @@ struct Engine {
   ZRec* d_carry[2] = {nullptr, nullptr};
   uint32_t* d_land_n[2] = {nullptr, nullptr};
   uint32_t* d_carry_n[2] = {nullptr, nullptr};
+  ZRec* d_S = nullptr;
   ORec* d_O = nullptr;
-  // pulled delivery (engine_dev.h EngDev::P...): send regions, tile
-  // directories, tile offsets and counts, records per zone; laid out for p_nz
-  // zones (the directory's bucket order depends on the zone count)
-  ZRec* d_P[2] = {nullptr, nullptr};
-  uint16_t* d_pdir[2] = {nullptr, nullptr};
-  uint32_t* d_ptbase[2] = {nullptr, nullptr};
-  uint32_t* d_pntile[2] = {nullptr, nullptr};
-  uint32_t* d_pn[2] = {nullptr, nullptr};
-  uint32_t p_nz = 0, pcap = 0, tcap = 0, nbp = 0, nper = 0, lds_region = 0;
-  // per-step record index pool of k_step (u32 words) and its two cursors
-  uint32_t* d_gi = nullptr;
-  unsigned long long* d_gi_n = nullptr;
-  uint64_t gi_cap = 0;
   uint32_t par = 0;                     // parity the next step reads
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_pend = nullptr;
@@ -388,14 +376,7 @@ int upload_types()
     e.land[p] = g.d_land[p]; e.carry[p] = g.d_carry[p];
     e.land_n[p] = g.d_land_n[p]; e.carry_n[p] = g.d_carry_n[p];
   }
-  e.O = g.d_O;
-  for(int p = 0; p < 2; ++p)
-  {
-    e.P[p] = g.d_P[p]; e.pdir[p] = g.d_pdir[p]; e.ptbase[p] = g.d_ptbase[p];
-    e.pntile[p] = g.d_pntile[p]; e.pn[p] = g.d_pn[p];
-  }
-  e.pcap = g.pcap; e.nbp = g.nbp; e.nper = g.nper;
-  e.gi = g.d_gi; e.gi_n = g.d_gi_n; e.gi_cap = g.gi_cap;
+  e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
   e.seq_max = R() > 1 ? kXSeqMax : kSeqMax;
@@ -520,79 +501,10 @@ int fixup_spill()
 // Re-lay the zone buffers after actors were created: zone z holds
 // Σ_{serial actors in z} cap(type) records. Capacities only grow, so mail
 // already landed or carried is copied zone by zone into the new layout.
-// Records in the send regions (parity g.par) moved into the landing buffers,
-// and every region emptied: before a k_sparse launch (it reads landing
-// buffers only) and before the zone count changes.
-int pull_to_landing()
-{
-  if(!g.d_pntile[0] || g.p_nz == 0) return 0;
-  hipLaunchKernelGGL(k_pull_land, dim3(g.p_nz * kMaxT), dim3(kBlock), 0, g.stream, g.par);
-  HIPCK(hipGetLastError());
-  for(int p = 0; p < 2; ++p)
-  {
-    HIPCK(hipMemsetAsync(g.d_pntile[p], 0, g.p_nz * sizeof(uint32_t), g.stream));
-    HIPCK(hipMemsetAsync(g.d_pn[p], 0, g.p_nz * sizeof(uint32_t), g.stream));
-    HIPCK(hipMemsetAsync(g.d_pdir[p], 0, (uint64_t)g.p_nz * kMaxT * (g.nbp + 2) * sizeof(uint16_t),
-      g.stream));
-  }
-  return 0;
-}
-
-// Send regions, directories and the LDS carve of k_step for nz zones.
-int alloc_pull(uint32_t nz)
-{
-  if(nz == g.p_nz && g.d_P[0]) return 0;
-  int rc = pull_to_landing();
-  if(rc) return rc;
-  HIPCK(hipStreamSynchronize(g.stream));
-  for(int p = 0; p < 2; ++p)
-  {
-    if(g.d_P[p]) HIPCK(hipFree(g.d_P[p]));
-    if(g.d_pdir[p]) HIPCK(hipFree(g.d_pdir[p]));
-    if(g.d_ptbase[p]) HIPCK(hipFree(g.d_ptbase[p]));
-    if(g.d_pntile[p]) HIPCK(hipFree(g.d_pntile[p]));
-    if(g.d_pn[p]) HIPCK(hipFree(g.d_pn[p]));
-    g.d_P[p] = nullptr; g.d_pdir[p] = nullptr; g.d_ptbase[p] = nullptr;
-    g.d_pntile[p] = nullptr; g.d_pn[p] = nullptr;
-  }
-  const uint32_t nbk = nz + (R() > 1 ? R() : 0u);
-  g.nper = (nz + 7u) / 8u;
-  g.nbp = 8u * g.nper;
-  // k_step's LDS region (zone_dev.h carve), the larger of the two layouts
-  // (with fan-in accumulators or without): the tile must hold a record per
-  // thread and the hot-group sort its work area
-  g.lds_region = step_region(true, nbk, g.nbp);
-  if(g.lds_region + std::max<uint32_t>(step_region_min(), 8u * al4(nbk)) > kLdsDyn)
-    return GPU_ACTOR_ERANGE;
-  g.tcap = step_tiled(false, nbk, g.nbp)
-           ? std::min<uint32_t>(step_tcap(kLdsDyn - step_region(false, nbk, g.nbp)),
-                                (uint32_t)(kFlPer * kZoneThreads))
-           : 0u;
-  g.pcap = std::max<uint32_t>((kMaxT * g.tcap + 15u) & ~15u, 16u);
-  const uint64_t ntile = (uint64_t)std::max<uint32_t>(nz, 1) * kMaxT;
-  for(int p = 0; p < 2; ++p)
-  {
-    HIPCK(hipMalloc(&g.d_P[p], (uint64_t)std::max<uint32_t>(nz, 1) * g.pcap * sizeof(ZRec)));
-    HIPCK(hipMalloc(&g.d_pdir[p], ntile * (g.nbp + 2) * sizeof(uint16_t)));
-    HIPCK(hipMemsetAsync(g.d_pdir[p], 0, ntile * (g.nbp + 2) * sizeof(uint16_t), g.stream));
-    HIPCK(hipMalloc(&g.d_ptbase[p], ntile * sizeof(uint32_t)));
-    HIPCK(hipMalloc(&g.d_pntile[p], std::max<uint32_t>(nz, 1) * sizeof(uint32_t)));
-    HIPCK(hipMalloc(&g.d_pn[p], std::max<uint32_t>(nz, 1) * sizeof(uint32_t)));
-    HIPCK(hipMemsetAsync(g.d_pntile[p], 0, std::max<uint32_t>(nz, 1) * sizeof(uint32_t), g.stream));
-    HIPCK(hipMemsetAsync(g.d_pn[p], 0, std::max<uint32_t>(nz, 1) * sizeof(uint32_t), g.stream));
-  }
-  g.p_nz = nz;
-  return 0;
-}
-
 int relayout_zones()
 {
   const uint32_t nz = (uint32_t)((g.n_local + kZone - 1) / kZone);
   if(nz > kMaxZones) return GPU_ACTOR_ERANGE;
-  {
-    const int prc = alloc_pull(nz);
-    if(prc) return prc;
-  }
   std::vector<uint64_t> cap64(nz, 0);
   for(const HostType& t : g.types)
   {
@@ -653,29 +565,12 @@ int relayout_zones()
     if(g.d_carry_n[p]) HIPCK(hipFree(g.d_carry_n[p]));
     g.d_land[p] = land; g.d_carry[p] = carry; g.d_land_n[p] = ln; g.d_carry_n[p] = cn;
   }
+  if(g.d_S) HIPCK(hipFree(g.d_S));
   if(g.d_O) HIPCK(hipFree(g.d_O));
   if(g.d_zoff) HIPCK(hipFree(g.d_zoff));
   if(g.d_zcap) HIPCK(hipFree(g.d_zcap));
+  HIPCK(hipMalloc(&g.d_S, 3 * bytes));     // 2 x: records of a zone; 1 x: sort scratch
   HIPCK(hipMalloc(&g.d_O, std::max<uint64_t>(total, 16) * sizeof(ORec)));
-  // the record-index pool: a step has at most every carried, landed and
-  // pulled record in flight (bound); GI takes one word per record and a hot
-  // receiver's sort at most five more
-  {
-    const uint64_t bound = 2ull * total + (uint64_t)nz * g.pcap + 2ull * nz;
-    const uint64_t want = 6ull * bound + 64;
-    if(want > g.gi_cap)
-    {
-      if(g.d_gi) HIPCK(hipFree(g.d_gi));
-      g.d_gi = nullptr;
-      HIPCK(hipMalloc(&g.d_gi, want * sizeof(uint32_t)));
-      g.gi_cap = want;
-    }
-    if(!g.d_gi_n)
-    {
-      HIPCK(hipMalloc(&g.d_gi_n, 2 * sizeof(unsigned long long)));
-      HIPCK(hipMemsetAsync(g.d_gi_n, 0, 2 * sizeof(unsigned long long), g.stream));
-    }
-  }
   g.d_zoff = d_off;
   g.d_zcap = d_cap;
   g.zone_records = total;
@@ -1042,30 +937,10 @@ int spawn_process(uint32_t cur)
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
-  // every byte of the CU's LDS: the carve of zone_dev.h (fixed part, bucket
-  // arrays, then the shared region that holds the drain rounds' tile)
-  const size_t dyn = kLdsDyn;
+  // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
+  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
+                                                          kSortWork);
   step_kernel_t kern = pick_step_kernel();
-  {
-    static step_kernel_t attr_set[32];
-    static int n_attr = 0;
-    bool known = false;
-    for(int i = 0; i < n_attr; ++i) known |= attr_set[i] == kern;
-    if(!known)
-    {
-      hipFuncAttributes fa;
-      HIPCK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)));
-      if(fa.sharedSizeBytes > kLdsStatic)
-      {
-        fprintf(stderr, "gpu_actor: k_step uses %zu B of static LDS (> %u)\n", fa.sharedSizeBytes,
-          kLdsStatic);
-        return GPU_ACTOR_EHIP;
-      }
-      HIPCK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-      if(n_attr < 32) attr_set[n_attr++] = kern;
-    }
-  }
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
@@ -1150,17 +1025,8 @@ void free_all()
     if(g.d_land_n[p]) (void)hipFree(g.d_land_n[p]);
     if(g.d_carry_n[p]) (void)hipFree(g.d_carry_n[p]);
   }
+  if(g.d_S) (void)hipFree(g.d_S);
   if(g.d_O) (void)hipFree(g.d_O);
-  for(int p = 0; p < 2; ++p)
-  {
-    if(g.d_P[p]) (void)hipFree(g.d_P[p]);
-    if(g.d_pdir[p]) (void)hipFree(g.d_pdir[p]);
-    if(g.d_ptbase[p]) (void)hipFree(g.d_ptbase[p]);
-    if(g.d_pntile[p]) (void)hipFree(g.d_pntile[p]);
-    if(g.d_pn[p]) (void)hipFree(g.d_pn[p]);
-  }
-  if(g.d_gi) (void)hipFree(g.d_gi);
-  if(g.d_gi_n) (void)hipFree(g.d_gi_n);
   if(g.d_zoff) (void)hipFree(g.d_zoff);
   if(g.d_zcap) (void)hipFree(g.d_zcap);
   for(int p = 0; p < 2; ++p)
@@ -1315,8 +1181,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_stats, ST_COUNT * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats, 0, ST_COUNT * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
-  HIPCK(hipMalloc(&g.d_dbg, kMaxZones * 16 * sizeof(unsigned long long)));
-  HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * 16 * sizeof(unsigned long long), g.stream));
+  HIPCK(hipMalloc(&g.d_dbg, kMaxZones * 8 * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * 8 * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_spawn_n, sizeof(unsigned int)));
   HIPCK(hipMemsetAsync(g.d_spawn_n, 0, sizeof(unsigned int), g.stream));
   HIPCK(hipMalloc(&g.d_tstart, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
@@ -1418,14 +1284,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
     g.d_land[p] = g.d_carry[p] = nullptr;
     g.d_land_n[p] = g.d_carry_n[p] = nullptr;
   }
-  g.d_O = nullptr;
-  for(int p = 0; p < 2; ++p)
-  {
-    g.d_P[p] = nullptr; g.d_pdir[p] = nullptr; g.d_ptbase[p] = nullptr;
-    g.d_pntile[p] = nullptr; g.d_pn[p] = nullptr;
-  }
-  g.p_nz = g.pcap = g.tcap = g.nbp = g.nper = g.lds_region = 0;
-  g.d_gi = nullptr; g.d_gi_n = nullptr; g.gi_cap = 0;
+  g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
@@ -1700,8 +1559,6 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
         // few messages in flight: whole supersteps in one workgroup until the
         // world is quiet, max_steps, or a step needs the zone path
         SparseCtl c;
-        rc = pull_to_landing();
-        if(rc) return rc;
         rc = run_sparse(max_steps ? max_steps - done : 0, c);
         if(rc) return rc;
         done += c.steps;
@@ -1729,7 +1586,6 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       if(max_steps) k = (uint32_t)std::min<uint64_t>(k, max_steps - done);
       // pend[j] = pending at the start of step j (k_step), pend[k] = after the chunk
       HIPCK(hipMemsetAsync(g.d_pend, 0, (k + 1) * sizeof(unsigned long long), g.stream));
-      HIPCK(hipMemsetAsync(g.d_gi_n, 0, 2 * sizeof(unsigned long long), g.stream));
       for(uint32_t j = 0; j < k; ++j)
       {
         par_at[j] = g.par;
@@ -1864,7 +1720,6 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   while(left)
   {
     HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
-    HIPCK(hipMemsetAsync(g.d_gi_n, 0, 2 * sizeof(unsigned long long), g.stream));
     const uint32_t par0 = g.par, sidx0 = g.sidx;
     HIPCK(hipEventRecord(g.ev[0], g.stream));
     for(uint64_t j = 0; j < left; ++j)
@@ -2041,7 +1896,7 @@ GPU_ACTOR_API int gpu_actor_debug_stamps(uint64_t* out, uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init || !out) return GPU_ACTOR_ESTATE;
-  n = std::min<uint64_t>(n, (uint64_t)kMaxZones * 16);
+  n = std::min<uint64_t>(n, (uint64_t)kMaxZones * 8);
   HIPCK(hipMemcpyAsync(out, g.d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   return 0;

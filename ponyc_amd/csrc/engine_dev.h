@@ -117,26 +117,8 @@ struct EngDev {
   ZRec* carry[2];
   uint32_t* land_n[2];            // [n_zones]
   uint32_t* carry_n[2];
-  ORec* O;                        // zone z: [zoff[z], zoff[z] + zcapz[z]) (remote / overflow sends)
-  // pulled delivery: zone s's sends of the step that writes
-  // parity p, one LDS-sorted tile per drain round, in P[p][s * pcap ...];
-  // tile t's bucket starts (XCD-major bucket order, nbp + 1 u16) in
-  // pdir[p][(s * kMaxT + t) * (nbp + 1)], its offset in ptbase, the tile count
-  // in pntile and the records in pn
-  ZRec* P[2];
-  uint16_t* pdir[2];
-  uint32_t* ptbase[2];
-  uint32_t* pntile[2];
-  uint32_t* pn[2];
-  uint32_t pcap;                  // records per send region (kMaxT tiles)
-  uint32_t nbp, nper;             // XCD-major bucket slots (8 * nper), zones per XCD slot
-  uint32_t pad5;
-  // per-step record index of each zone (u32 entries into carry / landing / P)
-  // and hot-receiver sort scratch, bump-allocated from one pool; gi_n[k & 1]
-  // is the cursor of step k
-  uint32_t* gi;
-  unsigned long long* gi_n;
-  unsigned long long gi_cap;
+  ZRec* S;                        // zone z: [3 zoff[z], 3 zoff[z] + 3 zcapz[z])
+  ORec* O;                        // zone z: [zoff[z], zoff[z] + zcapz[z])
   unsigned long long* stats;
   unsigned long long* pend;       // per-step pending counters
   XRec*  xout;                    // [nranks][xcap]
@@ -275,18 +257,13 @@ struct ActorBase {
 struct ZoneCtx;
 __device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg);
 
-__device__ __forceinline__ void tile_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg);
-
 struct ZoneCtx : ActorBase {
-  ORec*     out;         // zone outbox (global scratch): remote and overflow sends
+  ORec*     out;         // zone outbox (global scratch)
   uint32_t  ocap;        // its capacity
   uint32_t  nxt;         // landing parity of this step's sends
   uint32_t* s_nout;      // LDS outbox counter
-  uint32_t* s_hist;      // LDS histogram by bucket (outbox records)
-  uint4*    s_tile;      // LDS tile of this round's local sends (outbox format)
-  uint32_t* s_tn;        // tile fill (may pass tcap: the rest go to the outbox)
-  uint32_t  tcap;
-  __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg) { tile_put(*this, to, w, arg); }
+  uint32_t* s_hist;      // LDS histogram by bucket
+  __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg) { outbox_put(*this, to, w, arg); }
 };
 // ---- delivery --------------------------------------------------------------
 
@@ -340,11 +317,6 @@ __device__ __forceinline__ void land_store(uint32_t p, uint32_t z, uint32_t pos,
     spill_rec(p, 0u, z, pos, v);
 }
 
-__device__ __forceinline__ bool is_remote(uint32_t to)
-{
-  return c_eng.nranks > 1 && rmod(to) != c_eng.rank;
-}
-
 // Outbox full (a zone sent more than its mailbox capacity this step): land the
 // record directly with its own atomic on the destination bucket's counter. The
 // receiver sorts by key, so where a record lands does not change delivery order.
@@ -388,36 +360,6 @@ __device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, 
   r.to = to; r.w = w | a.src_local; r.arg = arg;
   *reinterpret_cast<uint4*>(a.out + idx) = *reinterpret_cast<const uint4*>(&r);
   atomicAdd(&a.s_hist[bucket_of(to)], 1u);
-}
-
-// XCD-major bucket slot of destination zone b: zones z = x (mod 8) run on XCD
-// x, so the receivers one XCD runs read one contiguous stretch of each tile
-// (and of its directory) and share its boundary lines in their own L2.
-__device__ __forceinline__ uint32_t xcd_slot(uint32_t b, uint32_t nper)
-{
-  return (b & 7u) * nper + (b >> 3);
-}
-
-// A send to a local actor goes to this round's LDS tile (sorted by bucket and
-// written to the zone's send region when the round ends); remote sends and
-// sends past the tile's capacity go to the outbox.
-__device__ __forceinline__ void tile_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg)
-{
-  if(!is_remote(to))
-  {
-    const uint32_t slot = atomicAdd(a.s_tn, 1u);
-    if(slot < a.tcap)
-    {
-      uint4 v;
-      v.x = to;
-      v.y = w | a.src_local;
-      v.z = (uint32_t)arg;
-      v.w = (uint32_t)(arg >> 32);
-      a.s_tile[slot] = v;
-      return;
-    }
-  }
-  outbox_put(a, to, w, arg);
 }
 
 // A handler's send: stamped with its canonical (sender, seq) key now.
@@ -475,6 +417,10 @@ __device__ __forceinline__ void spawn_actor(A& a, uint32_t type, uint32_t beh, u
   a.seq++;
 }
 
+__device__ __forceinline__ bool is_remote(uint32_t to)
+{
+  return c_eng.nranks > 1 && rmod(to) != c_eng.rank;
+}
 
 // fan-in Analyzer apply, aggregated per wavefront: lanes hitting the same
 // analyzer fold their count and XOR through LDS and one lane issues the two

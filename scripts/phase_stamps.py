@@ -2,9 +2,8 @@
 
 Runs the bench workload for a few steps and prints, per phase, the median over
 zones of the shader-clock cycles between the stamps (zone_dev.h GPA_STAMP):
-  0->1 directory (segments pulled)   1->2 count   2->3 scans + index allocation
-  3->4 place   4->5 handlers + tile flushes   5->6 carry-out, trigger bytes
-  6->7 outbox (remote / overflow) + counters
+  0->1 count   1->2 scans   2->3 place into S   3->4 carry-out scan + handlers
+  4->5 chunk reservation   5->6 outbox scatter + counters
 Only shares are meaningful (stamps perturb the kernel).
 """
 import ctypes
@@ -35,24 +34,16 @@ lib = eng.lib
 lib.gpu_actor_debug_stamps.restype = ctypes.c_int
 lib.gpu_actor_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nz = (N + 2047) // 2048
-buf = np.zeros(nz * 16, dtype=np.uint64)
+buf = np.zeros(nz * 8, dtype=np.uint64)
 lib.gpu_actor_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-st = buf.reshape(nz, 16).astype(np.int64)
-names = ["directory", "count", "scans", "place", "handlers", "carry-out", "outbox"]
-d = np.diff(st[:, :8], axis=1)
-tot = st[:, 7] - st[:, 0]
+st = buf.reshape(nz, 8).astype(np.int64)
+names = ["count", "scans", "place S", "handlers", "reserve", "scatter"]
+d = np.diff(st[:, :7], axis=1)
+tot = st[:, 6] - st[:, 0]
 print(f"zones={nz} median zone span={np.median(tot):.0f} clk; drain_ms={eng.last_drain_ms():.4f}")
 for i, nm in enumerate(names):
     print(f"  {nm:10s} median {np.median(d[:, i]):9.0f} clk  share {np.median(d[:, i] / tot):.3f}")
-# inside the handler phase: drain round r ends at stamp 8 + 2r, its flush at 9 + 2r
-prev = st[:, 4]
-for r in range(4):
-    a, b = 8 + 2 * r, 9 + 2 * r
-    if not st[:, a].any():
-        break
-    print(f"    round {r}: drain {np.median(st[:, a] - prev):8.0f} clk  flush {np.median(st[:, b] - st[:, a]):8.0f} clk")
-    prev = st[:, b]
 # launch skew: when zones start relative to the first
 start = st[:, 0] - st[:, 0].min()
-print(f"  zone start skew: median {np.median(start):.0f} max {start.max():.0f} clk; span max {tot.max():.0f}")
+print(f"  zone start skew: median {np.median(start):.0f} max {start.max():.0f} clk")
 eng.shutdown()
