@@ -126,6 +126,17 @@ GPU_ACTOR_API int gpu_actor_type_register(uint32_t type_id, uint32_t state_words
  * ring capacity (power of two). 0 keeps the config default. */
 GPU_ACTOR_API int gpu_actor_type_config(uint32_t type_id, uint32_t batch,
   uint32_t mailbox_cap);
+/* Per-type scheduling priority (the fork's _priority() hint, actor.c:414-416;
+ * default PONY_DEFAULT_ACTOR_PRIORITY = 0, scheduler.h:20). In the reference a
+ * rescheduled actor whose priority exceeds the next runnable actor's keeps its
+ * scheduler thread and runs its next batch at once (scheduler.c:1053-1068);
+ * every default actor ranks below a positive priority. Restated per
+ * superstep: an actor of a type with priority > 0 runs batch after batch
+ * while mail is pending at the step's start — it handles all of it unless a
+ * behaviour mutes it or yields — and is overloaded afterwards iff its last
+ * batch was full (handled a positive multiple of its batch) and it was not
+ * muted. Priorities <= 0 keep one batch per step. Any time between runs. */
+GPU_ACTOR_API int gpu_actor_type_priority(uint32_t type_id, int32_t priority);
 /* Handler-table parameter `idx` (< GPU_ACTOR_MAX_PARAMS) of a type; set before
  * gpu_actor_create, which runs the table's constructor with them. */
 GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value);

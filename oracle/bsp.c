@@ -48,6 +48,7 @@ typedef struct {
 typedef struct {
   int      registered, created;
   uint32_t words, ht, batch, cap, reducible;
+  int32_t  priority;      /* the fork's _priority() hint (actor.c:414-416)   */
   uint64_t params[GPU_ACTOR_MAX_PARAMS];
   uint64_t first, count;  /* id range [first, first + count): created + reserve */
   uint64_t live;          /* created + spawned so far                        */
@@ -148,6 +149,15 @@ int or_type_config(uint32_t type_id, uint32_t batch, uint32_t cap)
   if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered) return GPU_ACTOR_EINVAL;
   if(batch) S.types[type_id].batch = batch;
   if(cap) S.types[type_id].cap = cap;
+  return 0;
+}
+
+/* scheduler.c:1053-1068: a rescheduled actor that outranks the next runnable
+ * one keeps running; every default (0) actor ranks below a positive priority */
+int or_type_priority(uint32_t type_id, int32_t priority)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered) return GPU_ACTOR_EINVAL;
+  S.types[type_id].priority = priority;
   return 0;
 }
 
@@ -563,9 +573,12 @@ static void trig_set(uint64_t a, int v)
  *   - an actor runs min(batch, mail at step start) messages and stops early
  *     after a message whose sends muted it (send()) or that yielded
  *     (ponyint_actor_yield, actor.c:675-679); the rest waits, in order;
- *   - it is overloaded after the step iff it ran a full batch and was not
- *     muted (batch_limit_reached, actor.c:369-381); an actor that did not run
- *     is not overloaded. */
+ *   - an actor of a type with priority > 0 runs batch after batch
+ *     (scheduler.c:1053-1068 keeps it running while it outranks the next
+ *     runnable actor): all the mail at step start, with the same early stops;
+ *   - it is overloaded after the step iff it ran a full batch (a priority
+ *     type: its last batch) and was not muted (batch_limit_reached,
+ *     actor.c:369-381); an actor that did not run is not overloaded. */
 static void run_step(void)
 {
   typedef struct { uint64_t a; int t; } upd_t;
@@ -593,7 +606,7 @@ static void run_step(void)
       {
         f->m = 0;
         const uint64_t avail = (m->stamp == S.steps + 1 ? m->tail0 : m->tail) - m->head;
-        const uint64_t w_ = avail < t->batch ? avail : t->batch;
+        const uint64_t w_ = (t->priority > 0 || avail < t->batch) ? avail : t->batch;
         S.cur = a; S.cur_prev_o = prev_o; S.mute_hit = 0; S.yield_req = 0;
         for(uint64_t k = 0; k < w_; k++)
         {
@@ -609,7 +622,9 @@ static void run_step(void)
         if(S.mute_hit) { muted_now = 1; f->r = (uint32_t)S.mute_to; }
       }
       f->m = (uint8_t)muted_now;
-      f->o = (uint8_t)(handled == t->batch && !muted_now);
+      const int full = t->priority > 0 ? (handled != 0 && handled % t->batch == 0)
+                                       : handled == t->batch;
+      f->o = (uint8_t)(full && !muted_now);
       if(n_upd == upd_alloc)
       {
         upd_alloc = upd_alloc ? 2 * upd_alloc : 1024;

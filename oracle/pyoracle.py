@@ -45,6 +45,7 @@ def load():
         "or_init": (i32, [u32]), "or_shutdown": (None, []),
         "or_type_register": (i32, [u32, u32, u32]),
         "or_type_config": (i32, [u32, u32, u32]),
+        "or_type_priority": (i32, [u32, ctypes.c_int32]),
         "or_type_param": (i32, [u32, u32, u64]),
         "or_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
         "or_type_reserve": (i32, [u32, u64]),
@@ -97,6 +98,9 @@ class Oracle:
 
     def type_config(self, type_id, batch=0, mailbox_cap=0):
         _ck("or_type_config", self.lib.or_type_config(type_id, batch, mailbox_cap))
+
+    def type_priority(self, type_id, priority):
+        _ck("or_type_priority", self.lib.or_type_priority(type_id, priority))
 
     def type_param(self, type_id, idx, value):
         _ck("or_type_param", self.lib.or_type_param(type_id, idx, int(value) & U64))

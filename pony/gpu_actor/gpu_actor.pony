@@ -21,6 +21,7 @@ use @gpu_actor_shutdown[I32]()
 use @gpu_actor_comm_id[I32](out128: Pointer[U8] tag)
 use @gpu_actor_type_register[I32](type_id: U32, state_words: U32, table: U32)
 use @gpu_actor_type_config[I32](type_id: U32, batch: U32, mailbox_cap: U32)
+use @gpu_actor_type_priority[I32](type_id: U32, priority: I32)
 use @gpu_actor_type_param[I32](type_id: U32, idx: U32, value: U64)
 use @gpu_actor_create[I32](type_id: U32, count: U64, first: Pointer[U64])
 use @gpu_actor_type_reserve[I32](type_id: U32, n: U64)
@@ -176,6 +177,10 @@ class GpuActors
   fun config(type_id: U32, batch: U32, mailbox_cap: U32 = 0): I32 =>
     """The fork's _batch() hint (actor.c:410-416) and the zone sizing hint."""
     @gpu_actor_type_config(type_id, batch, mailbox_cap)
+
+  fun priority(type_id: U32, priority': I32): I32 =>
+    """The fork's _priority() hint (actor.c:414-416, scheduler.c:1053-1068)."""
+    @gpu_actor_type_priority(type_id, priority')
 
   fun send(to: U64, behaviour: U32, arg: U64): I32 =>
     """pony_sendi: staged on the host, injected by the next run (no sync)."""

@@ -202,6 +202,7 @@ struct HostType {
   uint64_t first = 0, count = 0;
   uint32_t lfirst = 0, lcount = 0;
   uint64_t reserve = 0;                 // ids for actors spawned by behaviours
+  int32_t priority = 0;                 // the fork's _priority() hint
   uint64_t* d_state = nullptr;
 };
 
@@ -361,6 +362,7 @@ int upload_types()
     d.lfirst = h.lfirst; d.lcount = h.lcount;
     d.ht = h.ht; d.words = h.words; d.batch = h.batch; d.cap = h.cap;
     d.reducible = reducible_ht(h.ht);
+    d.prio = h.priority > 0 ? 1u : 0u;
     d.state = h.d_state;
     memcpy(d.params, h.params, sizeof(d.params));
   }
@@ -1350,6 +1352,16 @@ GPU_ACTOR_API int gpu_actor_type_config(uint32_t type_id, uint32_t batch, uint32
   if(batch) t.batch = batch;
   if(mailbox_cap) t.cap = mailbox_cap;
   return t.created ? upload_types() : 0;
+}
+
+GPU_ACTOR_API int gpu_actor_type_priority(uint32_t type_id, int32_t priority)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init) return GPU_ACTOR_ESTATE;
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !g.types[type_id].registered) return GPU_ACTOR_EINVAL;
+  if(g.async_busy) return GPU_ACTOR_EBUSY;
+  g.types[type_id].priority = priority;
+  return g.types[type_id].created ? upload_types() : 0;
 }
 
 GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value)

@@ -102,7 +102,7 @@ struct TypeDev {
   uint32_t first, count;     // global id range
   uint32_t lfirst, lcount;   // local slot range on this rank
   uint32_t ht, words, batch, cap;
-  uint32_t reducible, pad;
+  uint32_t reducible, prio;   // prio: priority > 0 (gpu_actor_type_priority)
   uint64_t* state;           // [words][lcount]
   uint64_t  params[GPU_ACTOR_MAX_PARAMS];
 };

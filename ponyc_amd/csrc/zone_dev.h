@@ -274,7 +274,8 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   const TypeDev T = Tref;
   constexpr int NW = HT_Words<HT>::W;
   constexpr bool kY = may_yield<HT>();
-  const uint32_t w = n < T.batch ? n : T.batch;
+  // a priority type runs batch after batch: everything pending
+  const uint32_t w = (T.prio || n < T.batch) ? n : T.batch;
   uint64_t s[NW];
 #pragma unroll
   for(int k = 0; k < NW; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
@@ -876,9 +877,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
     }
 #undef ZDRAIN
-    // overloaded iff a full batch ran and the actor was not muted
-    // (batch_limit_reached, actor.c:369-381; maybe_mute first, 449-460)
-    const uint32_t o = (d == T.batch && !a.mute_hit) ? 1u : 0u;
+    // overloaded iff a full batch ran (a priority type's last batch) and the
+    // actor was not muted (batch_limit_reached, actor.c:369-381; maybe_mute
+    // first, 449-460)
+    const bool full = T.prio ? (d != 0u && d % T.batch == 0u) : d == T.batch;
+    const uint32_t o = (full && !a.mute_hit) ? 1u : 0u;
     const uint32_t m = (stays || a.mute_hit) ? 1u : 0u;
     if(a.mute_hit) c_eng.muted_on[L] = a.mute_to;
     const uint32_t nb_ = o | (m << 1);

@@ -76,7 +76,8 @@ class Counts(ctypes.Structure):
 # every symbol include/gpu_actor.h declares
 EXPORTS = [
     "gpu_actor_init", "gpu_actor_shutdown", "gpu_actor_comm_id",
-    "gpu_actor_type_register", "gpu_actor_type_config", "gpu_actor_type_param",
+    "gpu_actor_type_register", "gpu_actor_type_config", "gpu_actor_type_priority",
+    "gpu_actor_type_param",
     "gpu_actor_create", "gpu_actor_type_reserve", "gpu_actor_type_live",
     "gpu_actor_alloc_msgs", "gpu_actor_sendv", "gpu_actor_send",
     "gpu_actor_run", "gpu_actor_run_fixed", "gpu_actor_sync",
@@ -116,6 +117,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "gpu_actor_comm_id": (i32, [vp]),
         "gpu_actor_type_register": (i32, [u32, u32, u32]),
         "gpu_actor_type_config": (i32, [u32, u32, u32]),
+        "gpu_actor_type_priority": (i32, [u32, ctypes.c_int32]),
         "gpu_actor_type_param": (i32, [u32, u32, u64]),
         "gpu_actor_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
         "gpu_actor_type_reserve": (i32, [u32, u64]),
@@ -242,6 +244,10 @@ class Engine:
 
     def type_config(self, type_id: int, batch: int = 0, mailbox_cap: int = 0) -> None:
         _ck("gpu_actor_type_config", self.lib.gpu_actor_type_config(type_id, batch, mailbox_cap))
+
+    def type_priority(self, type_id: int, priority: int) -> None:
+        """The fork's _priority() hint (include/gpu_actor.h)."""
+        _ck("gpu_actor_type_priority", self.lib.gpu_actor_type_priority(type_id, priority))
 
     def type_param(self, type_id: int, idx: int, value: int) -> None:
         _ck("gpu_actor_type_param",

@@ -192,17 +192,20 @@ def spreader_result(eng, w: dict) -> np.ndarray:
 # ---- per-pair FIFO probe ---------------------------------------------------------------------
 def fifo(eng, sources: int = 64, sinks: int = 8, bursts: int = 10, m: int = 4,
          sink_type: int = 0, src_type: int = 1, batch: int = 0, mailbox_cap: int = 0,
-         sink_yield: int = 0) -> dict:
+         sink_yield: int = 0, sink_priority: int = 0) -> dict:
     """Per-pair FIFO probe (include/gpu_actor.h HT_FIFO_SRC/SINK): `sources`
     actors burst m PUSHes each to sink i % sinks, `bursts` times. The sink's
     fold is order-sensitive; `sink_yield` > 0 makes it yield after every k-th
-    message (ponyint_actor_yield). The shape of examples/overload (many
-    senders, one slow receiver) when sources >> sinks."""
+    message (ponyint_actor_yield); `sink_priority` is the sinks' _priority()
+    hint. The shape of examples/overload (many senders, one slow receiver)
+    when sources >> sinks."""
     eng.type_register(sink_type, 11, HT_FIFO_SINK)
     if batch or mailbox_cap:
         eng.type_config(sink_type, batch, mailbox_cap)
     eng.type_param(sink_type, 0, sinks)
     eng.type_param(sink_type, 1, sink_yield)
+    if sink_priority:
+        eng.type_priority(sink_type, sink_priority)
     kfirst = eng.create(sink_type, sinks)
     eng.type_register(src_type, 3, HT_FIFO_SRC)
     eng.type_param(src_type, 0, kfirst)

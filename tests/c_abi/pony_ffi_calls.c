@@ -30,6 +30,7 @@ int32_t gpu_actor_shutdown(void);
 int32_t gpu_actor_comm_id(void* out128);
 int32_t gpu_actor_type_register(uint32_t type_id, uint32_t state_words, uint32_t table);
 int32_t gpu_actor_type_config(uint32_t type_id, uint32_t batch, uint32_t mailbox_cap);
+int32_t gpu_actor_type_priority(uint32_t type_id, int32_t priority);
 int32_t gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
 int32_t gpu_actor_create(uint32_t type_id, uint64_t count, void* first);
 int32_t gpu_actor_type_reserve(uint32_t type_id, uint64_t n);
@@ -69,6 +70,7 @@ static int cpu_mode(void)
   EXPECT(gpu_actor_shutdown(), ESTATE);
   EXPECT(gpu_actor_type_register(0, 3, 2), ESTATE);
   EXPECT(gpu_actor_type_config(0, 100, 16), ESTATE);
+  EXPECT(gpu_actor_type_priority(0, 1), ESTATE);
   EXPECT(gpu_actor_type_param(0, 0, 1), ESTATE);
   EXPECT(gpu_actor_create(0, 1, &u), ESTATE);
   EXPECT(gpu_actor_type_reserve(0, 1), ESTATE);
@@ -125,6 +127,7 @@ static int gpu_mode(const char* out_path)
   /* message-ubench (examples/message-ubench/main.pony:223-286) */
   EXPECT(gpu_actor_type_register(0, 3, 2), 0);
   EXPECT(gpu_actor_type_config(0, 0, 16), 0);
+  EXPECT(gpu_actor_type_priority(0, 0), 0);
   EXPECT(gpu_actor_type_param(0, 0, N_PING), 0);
   EXPECT(gpu_actor_type_param(0, 2, 20), 0);
   EXPECT(gpu_actor_type_param(0, 3, 5489), 0);

@@ -75,3 +75,20 @@ def test_hot_receiver_group_sort(engine_factory, oracle, sources, m):
     _both(engine_factory, oracle,
           lambda e: W.fifo(e, sources, 2, 1, m, batch=1 << 20, mailbox_cap=16),
           W.fifo_result, mailbox_cap=16)
+
+
+@pytest.mark.parametrize("sources,sinks,bursts,m,batch,prio", [
+    (64, 7, 10, 4, 7, 1),       # a priority sink drains its whole mailbox every step
+    (64, 7, 10, 4, 7, -3),      # a negative priority keeps one batch per step
+    (700, 4, 3, 2, 10, 2),      # groups of 350: exactly-full last batches stay overloaded
+    (3000, 4, 2, 1, 100, 5),    # 750 arrivals per sink, sorted by the workgroup, run whole
+])
+def test_priority(engine_factory, oracle, sources, sinks, bursts, m, batch, prio):
+    """The fork's _priority() hint (actor.c:414-416; scheduler.c:1053-1068),
+    restated per superstep (include/gpu_actor.h gpu_actor_type_priority):
+    mute, overload and carry follow from the sinks draining batch after
+    batch."""
+    _both(engine_factory, oracle,
+          lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=16,
+                           sink_priority=prio),
+          W.fifo_result, mailbox_cap=16)
