@@ -151,7 +151,9 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
  * becomes [first, first + count + n). A spawned actor's id is assigned at the
  * end of the superstep that created it, in (creator id, creator send
  * sequence) order after the type's live actors; its constructor message is
- * delivered in the next superstep like any other send. Single rank only. */
+ * delivered in the next superstep like any other send. With n_ranks > 1
+ * every rank gathers every rank's spawn records and numbers them alike, so
+ * the ids equal a single rank's; the owner (id % n_ranks) lands the message. */
 GPU_ACTOR_API int gpu_actor_type_reserve(uint32_t type_id, uint64_t n);
 /* Live (created + spawned) actors of a type. */
 GPU_ACTOR_API int gpu_actor_type_live(uint32_t type_id, uint64_t* live);
