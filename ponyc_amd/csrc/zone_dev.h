@@ -176,6 +176,31 @@ __device__ uint32_t block_scan_n(const uint32_t* in, uint32_t* out, uint32_t n, 
   return total;
 }
 
+// Add 1 to ctr[key] for every valid lane and return each lane's rank among
+// the lanes that added to the same counter (atomicAdd's return, in lane
+// order). The lanes of up to 4 distinct keys per wave are folded into one LDS
+// atomic each (carried backlogs, grouped by actor); the rest add one by one.
+__device__ __forceinline__ uint32_t agg_add(uint32_t* ctr, uint32_t key, bool valid)
+{
+  const uint32_t lane = __lane_id();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t active = __ballot(valid);
+  uint32_t res = 0;
+  for(int it = 0; it < 4 && active; ++it)
+  {
+    const int leader = __ffsll((long long)active) - 1;
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const uint64_t peers = __ballot(valid && key == k) & active;
+    uint32_t base = 0;
+    if((int)lane == leader) base = atomicAdd(&ctr[k], (uint32_t)__popcll(peers));
+    base = (uint32_t)__shfl((int)base, leader);
+    if((peers >> lane) & 1ull) res = base + (uint32_t)__popcll(peers & lt);
+    active &= ~peers;
+  }
+  if((active >> lane) & 1ull) res = atomicAdd(&ctr[key], 1u);
+  return res;
+}
+
 // 16-B record moves built from their four words. Written this way, the
 // scatter tile's records stay in registers and go to LDS as one ds_write_b128
 // each; the plain uint4 copy made the compiler split the LDS stores and spill
@@ -656,8 +681,21 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
   const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
   // carried records counted apart (s_ccnt); landed ones in s_cnt
-  for(uint32_t i = tid; i < nc; i += kZoneThreads)
-    atomicAdd(&s_ccnt[C[i].w0 & kZoneMask], 1u);
+  // carried mail is grouped by actor: a wave's lanes mostly share one
+  // counter (a backlog), folded into one atomic
+  for(uint32_t base = 0; base < nc; base += kZoneThreads * kUnroll)
+  {
+    uint32_t w[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t i = base + u * kZoneThreads + tid;
+      w[u] = i < nc ? C[i].w0 : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      (void)agg_add(s_ccnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
+  }
   // Landed records: with the LDS index, each record's rank among its actor's
   // arrivals comes back from the counting atomic and stays in a register
   // (packed rank << 11 | actor), so placing it needs no second pass over the
