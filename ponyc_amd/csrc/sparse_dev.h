@@ -53,6 +53,9 @@ struct SpList {
 __shared__ uint32_t sp_cnt[2];
 
 static_assert(kSpCap <= 1024, "packed rank counts hold 10-bit fields");
+static_assert(kSpCap <= kSpThreads, "one record per thread in the distinct-receiver check");
+constexpr uint32_t kSpHashBits = 13;       // receiver occupancy table (LDS, u32)
+constexpr uint32_t kSpHash = 1u << kSpHashBits;
 
 // per-type fields the sparse steps read, cached in LDS
 constexpr uint32_t kSpNoRun = 1u;     // reducible, or spawns actors: dense path only
@@ -179,6 +182,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
   __shared__ uint32_t s_over;
   __shared__ uint32_t s_acc[kSpThreads];        // packed rank counts (kSpCap <= kSpThreads)
   __shared__ SpType s_tinfo[GPU_ACTOR_MAX_TYPES];
+  __shared__ uint32_t s_hcnt[kSpHash];          // records per receiver hash this step
   __shared__ unsigned long long s_agg[kSpWaves];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
   __shared__ unsigned long long s_red[kSpWaves][4];
@@ -199,6 +203,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
   }
   if(tid == 0) { sp_cnt[0] = 0; sp_cnt[1] = 0; s_over = 0; }
   s_acc[tid] = 0;
+  for(uint32_t h = tid; h < kSpHash; h += kSpThreads) s_hcnt[h] = 0;
 
   // ---- gather landing[cur] into list 0 ---------------------------------------------
   // per-thread run of zones, exclusive scan of their record counts
@@ -276,6 +281,36 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     if(max_steps && steps >= max_steps) { reason = SP_MAX_STEPS; break; }
     const SpList Acur{bK[la], bW[la], bA[la]};
     const SpList Bnxt{bK[lb], bW[lb], bA[lb]};
+    // 0. every receiver distinct (a ring's tokens, one message per actor)? A
+    //    hashed occupancy count per receiver: no bucket above one means no
+    //    receiver has two records, so every record is a run of its own and the
+    //    order among runs is free — the rank sort is skipped. A collision
+    //    (or a real repeat) takes the sort.
+    uint32_t hb = 0;
+    if(tid < n)
+    {
+      hb = ((uint32_t)(Acur.K[tid] >> 32) * 0x9E3779B1u) >> (32 - kSpHashBits);
+      atomicAdd(&s_hcnt[hb], 1u);
+    }
+    __syncthreads();
+    const bool distinct = !__syncthreads_or(tid < n && s_hcnt[hb] > 1);
+    if(tid < n) s_hcnt[hb] = 0;              // read by every thread before the barrier above
+    int dense = 0;
+    uint32_t h_r = 0, h_g = 0;               // this thread's run: [h_r, h_r + h_g)
+    const SpList* Srun = &S;
+    if(distinct)
+    {
+      if(tid == 0) sp_cnt[q ^ 1u] = 0;       // the next step's counter, read last step
+      if(tid < n)
+      {
+        h_r = tid; h_g = 1;
+        const int t = sp_type(s_tinfo, n_types, (uint32_t)(Acur.K[tid] >> 32));
+        if(t < 0 || (s_tinfo[t].flags & kSpNoRun) || 1u >= s_tinfo[t].batch) dense = 1;
+      }
+      Srun = &Acur;
+    }
+    else
+    {
     // 1. canonical order. Record i's key (receiver, sender, seq) is compared
     //    with every other key by P threads, each over one slice of the list
     //    (consecutive lanes take consecutive records of the same slice, so
@@ -324,8 +359,6 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     // 2. place each record at its rank; the first record of each receiver's
     //    run (no lower key of the same receiver) owns the run. A run longer
     //    than its type's batch needs carry: the step goes to the dense path.
-    int dense = 0;
-    uint32_t h_r = 0, h_g = 0;               // this thread's run: [h_r, h_r + h_g)
     if(tid == 0) sp_cnt[q ^ 1u] = 0;         // the next step's counter, read last step
     if(tid < n)
     {
@@ -341,6 +374,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       }
     }
     s_acc[tid] = 0;                          // ready for the next step's counts
+    }
     const int any_dense = __syncthreads_or(dense);
     SP_STAMP(1);
     if(any_dense)
@@ -352,7 +386,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     //    run's behaviours in order and stores the state; sends go to list lb
     if(h_g)
     {
-      const uint32_t L = (uint32_t)(S.K[h_r] >> 32);
+      const SpList& Sr = *Srun;
+      const uint32_t L = (uint32_t)(Sr.K[h_r] >> 32);
       const int t = sp_type(s_tinfo, n_types, L);
       SparseCtx a;
       a.reset_common();
@@ -367,8 +402,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       // the usual case, one type for every run of the wave: its fields come
       // through scalar loads instead of a per-lane copy from constant memory
       const int tu = __builtin_amdgcn_readfirstlane(t);
-      if(__ballot(t != tu) == 0ull) sp_dispatch(c_types[tu], a, S, h_r, h_g, L);
-      else sp_dispatch(c_types[t], a, S, h_r, h_g, L);
+      if(__ballot(t != tu) == 0ull) sp_dispatch(c_types[tu], a, Sr, h_r, h_g, L);
+      else sp_dispatch(c_types[t], a, Sr, h_r, h_g, L);
       delivered += h_g;
       active += 1;
       sent += a.sent;
