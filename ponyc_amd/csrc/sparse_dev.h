@@ -286,27 +286,32 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     //    receiver has two records, so every record is a run of its own and the
     //    order among runs is free — the rank sort is skipped. A collision
     //    (or a real repeat) takes the sort.
+    // whether the record alone (a run of one) already needs the zone path
     uint32_t hb = 0;
+    int dense1 = 0;
     if(tid < n)
     {
-      hb = ((uint32_t)(Acur.K[tid] >> 32) * 0x9E3779B1u) >> (32 - kSpHashBits);
+      const uint32_t L = (uint32_t)(Acur.K[tid] >> 32);
+      hb = (L * 0x9E3779B1u) >> (32 - kSpHashBits);
       atomicAdd(&s_hcnt[hb], 1u);
+      const int t = sp_type(s_tinfo, n_types, L);
+      dense1 = (t < 0 || (s_tinfo[t].flags & kSpNoRun) || 1u >= s_tinfo[t].batch) ? 1 : 0;
     }
     __syncthreads();
-    const bool distinct = !__syncthreads_or(tid < n && s_hcnt[hb] > 1);
-    if(tid < n) s_hcnt[hb] = 0;              // read by every thread before the barrier above
+    const bool coll = tid < n && s_hcnt[hb] > 1;
+    // one barrier in the usual case (no repeat receiver, nothing for the zone
+    // path); a second tells a repeat from a dense record
+    const bool any_cd = __syncthreads_or(coll || dense1);
+    const bool distinct = !(any_cd && __syncthreads_or(coll));
+    if(tid < n) s_hcnt[hb] = 0;              // every read of it is behind the barriers above
     int dense = 0;
     uint32_t h_r = 0, h_g = 0;               // this thread's run: [h_r, h_r + h_g)
     const SpList* Srun = &S;
     if(distinct)
     {
       if(tid == 0) sp_cnt[q ^ 1u] = 0;       // the next step's counter, read last step
-      if(tid < n)
-      {
-        h_r = tid; h_g = 1;
-        const int t = sp_type(s_tinfo, n_types, (uint32_t)(Acur.K[tid] >> 32));
-        if(t < 0 || (s_tinfo[t].flags & kSpNoRun) || 1u >= s_tinfo[t].batch) dense = 1;
-      }
+      if(tid < n) { h_r = tid; h_g = 1; }
+      dense = any_cd ? 1 : 0;                // uniform: with no repeat, any_cd means a dense record
       Srun = &Acur;
     }
     else
@@ -375,7 +380,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     }
     s_acc[tid] = 0;                          // ready for the next step's counts
     }
-    const int any_dense = __syncthreads_or(dense);
+    const int any_dense = distinct ? dense : __syncthreads_or(dense);   // uniform either way
     SP_STAMP(1);
     if(any_dense)
     {
