@@ -287,23 +287,24 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     //    order among runs is free — the rank sort is skipped. A collision
     //    (or a real repeat) takes the sort.
     // whether the record alone (a run of one) already needs the zone path
+    // (the second record of a bucket sees a nonzero count come back from its
+    // add, so one OR over the workgroup tells whether any bucket repeats)
     uint32_t hb = 0;
     int dense1 = 0;
+    bool coll = false;
     if(tid < n)
     {
       const uint32_t L = (uint32_t)(Acur.K[tid] >> 32);
       hb = (L * 0x9E3779B1u) >> (32 - kSpHashBits);
-      atomicAdd(&s_hcnt[hb], 1u);
+      coll = atomicAdd(&s_hcnt[hb], 1u) != 0u;
       const int t = sp_type(s_tinfo, n_types, L);
       dense1 = (t < 0 || (s_tinfo[t].flags & kSpNoRun) || 1u >= s_tinfo[t].batch) ? 1 : 0;
     }
-    __syncthreads();
-    const bool coll = tid < n && s_hcnt[hb] > 1;
     // one barrier in the usual case (no repeat receiver, nothing for the zone
     // path); a second tells a repeat from a dense record
     const bool any_cd = __syncthreads_or(coll || dense1);
     const bool distinct = !(any_cd && __syncthreads_or(coll));
-    if(tid < n) s_hcnt[hb] = 0;              // every read of it is behind the barriers above
+    if(tid < n) s_hcnt[hb] = 0;              // every add to it is behind the barrier above
     int dense = 0;
     uint32_t h_r = 0, h_g = 0;               // this thread's run: [h_r, h_r + h_g)
     const SpList* Srun = &S;
