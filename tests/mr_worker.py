@@ -35,6 +35,9 @@ CASES = {
     "spreader": (lambda e: W.spreader(e, 10), W.spreader_result, {}),
     # backpressure across ranks: overloaded sinks mute senders on the other rank
     "mute": (lambda e: W.fifo(e, 600, 3, 3, 2, batch=10, mailbox_cap=16), W.fifo_result, {}),
+    # priority sinks drain batch after batch while their senders live on both ranks
+    "priority": (lambda e: W.fifo(e, 600, 3, 3, 2, batch=10, mailbox_cap=16, sink_priority=1),
+                 W.fifo_result, {}),
     # zone overflow on one rank halts the next step on every rank until grown
     "spill": (lambda e: W.fifo(e, 300, 3, 4, 9, batch=4, mailbox_cap=1), W.fifo_result,
               {"mailbox_cap": 1}),
