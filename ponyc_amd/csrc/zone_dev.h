@@ -830,6 +830,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       __syncthreads();
     }
   }
+  GPA_STAMP(7);                          // diagnostic build: the hot-group sort ends
   auto big_sorted = [&](uint32_t i) __attribute__((always_inline)) {
     return ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
   };
