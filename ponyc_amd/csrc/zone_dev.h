@@ -280,6 +280,9 @@ struct AccS {
   }
 };
 
+// Groups handled whole up to this size keep their keys in registers.
+constexpr uint32_t kMedReg = 16;
+
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
   return HT == GPU_ACTOR_HT_FIFO_SINK;
@@ -355,6 +358,30 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
         for(int j = 0; j < (int)SM; ++j)
           if((uint32_t)j == bi) k[j] = ~0ull;
         handle(HtTag<HT>{}, T, a, s, (uint32_t)best & 0xFu, barg);
+        ++done;
+        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
+      }
+    }
+    else if(SM < kMedReg && q >= g && g <= kMedReg && !presorted)
+    {
+      // medium group handled whole (more than the small path holds): keys in
+      // registers with the record's position in the low bits; each record is
+      // loaded again (a cache hit) when its turn comes
+      uint64_t km[kMedReg];
+#pragma unroll
+      for(int j = 0; j < (int)kMedReg; ++j)
+        km[j] = (uint32_t)j < g ? (zkey(acc.rec(nc + j)) << 4) | (uint64_t)j : ~0ull;
+      for(uint32_t r = 0; r < g && !stop; ++r)
+      {
+        uint64_t best = km[0];
+#pragma unroll
+        for(int j = 1; j < (int)kMedReg; ++j) best = km[j] < best ? km[j] : best;
+        const uint32_t bi = (uint32_t)best & 0xFu;
+#pragma unroll
+        for(int j = 0; j < (int)kMedReg; ++j)
+          if((uint32_t)j == bi) km[j] = ~0ull;
+        const ZRec rr = acc.rec(nc + bi);
+        handle(HtTag<HT>{}, T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg);
         ++done;
         stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
