@@ -55,7 +55,8 @@ static_assert(kTile % kZoneThreads == 0 && kIdxCap % kZoneThreads == 0, "tile / 
 // 128 VGPRs without spilling.
 template <int HT> __host__ __device__ constexpr uint32_t small_regs()
 {
-  return (HT == GPU_ACTOR_HT_PINGER || HT == GPU_ACTOR_HT_FANIN_SENDER) ? 16u : 8u;
+  return (HT == GPU_ACTOR_HT_PINGER || HT == GPU_ACTOR_HT_FANIN_SENDER ||
+          HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM) ? 16u : 8u;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
