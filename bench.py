@@ -32,6 +32,13 @@ Also reported on the same line:
                  the GPU (run to quiescence, median of 3) beside the same
                  reference harness at the same core counts (BASELINE names
                  "message-ubench & ring"; N=1 only).
+Ranks: `--gpus N` with N > 1 runs N rank processes, one per GPU. Under a
+launcher (torch.distributed.run: WORLD_SIZE set) WORLD_SIZE must equal N;
+without one, bench.py starts the N ranks itself (before any GPU call) and
+exits with the worst rank's status. The exchange is RCCL; if RCCL cannot be
+set up the run fails (non-zero exit) unless the host-staged exchange is asked
+for with --host-transport or PONYC_AMD_SAME_GPU=1 (every rank on device 0, a
+rehearsal of the N-rank path on a one-GPU box; `config.ranks_share_gpu`).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--actors A]
 """
 from __future__ import annotations
@@ -72,14 +79,63 @@ def parse():
     p.add_argument("--cpu-budget", type=int, default=10,
                    help="forward budget per pinger of the bounded CPU sample")
     p.add_argument("--cpu-runs", type=int, default=5)
+    p.add_argument("--host-transport", action="store_true",
+                   help="N > 1: exchange through pinned host memory + gloo instead of RCCL")
     return p.parse_args()
 
 
+def same_gpu() -> bool:
+    return os.environ.get("PONYC_AMD_SAME_GPU", "") not in ("", "0")
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """No launcher and --gpus N > 1: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets
+    them) and return the worst exit status. This process never touches the
+    GPU. If a rank fails, the others are stopped (they would wait forever at
+    the first collective)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    worst = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                worst = worst or (rc if rc > 0 else 128 - rc)
+                for q in live:          # exactly the processes started above
+                    q.kill()
+    return worst
+
+
 def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} "
+                         "(launch one rank per GPU, or run without a launcher)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("PONYC_AMD_SAME_GPU"):      # rehearsal: every rank on device 0
+    if same_gpu():      # rehearsal: every rank on device 0
         local = 0
     pg = None
     if world > 1:
@@ -252,32 +308,40 @@ def ring_gpu(reps: int = 3) -> dict:
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world, rank, local, pg = dist_setup(args)
     from ponyc_amd.engine import Engine, MSG_DTYPE, LIB_PATH
 
-    comm = None
-    if world > 1:
-        comm = bcast_bytes(pg, rank, Engine.comm_id() if rank == 0 else None)
+    host_xp = world > 1 and (args.host_transport or same_gpu())
     n_total = args.actors * world
     kw = dict(device=local, n_ranks=world, rank=rank, mailbox_cap=args.mailbox_cap,
               max_actors=n_total + 1024,
               max_exchange=max(1 << 20, 2 * args.actors * args.initial // max(world, 1)))
-    exchange = "none" if world == 1 else "rccl"
-    try:
-        eng = Engine(comm_id=comm, **kw)
-        ok = 1.0
-    except Exception as exc:        # RCCL unusable: say so, measure the host exchange
-        if world == 1:
-            raise
-        print(f"rank {rank}: RCCL exchange unavailable ({exc}); using the host transport",
-              file=sys.stderr)
-        ok = 0.0
-    if world > 1 and allmax(pg, 1.0 - ok) > 0:
-        if ok:
-            eng.shutdown()
+    if world == 1:
+        eng = Engine(**kw)
+        exchange = "none"
+    elif host_xp:
         from ponyc_amd.dist import GlooTransport
         eng = Engine(transport=GlooTransport(), **kw)
-        exchange = "host-staged (gloo)"
+        exchange = "host-staged"
+    else:
+        import torch
+        ndev = torch.cuda.device_count()      # counts devices without initialising HIP
+        if ndev < world:
+            raise SystemExit(f"bench.py: {world} ranks need {world} GPUs, this node has {ndev} "
+                             "(PONYC_AMD_SAME_GPU=1 rehearses N ranks on one GPU)")
+        comm = bcast_bytes(pg, rank, Engine.comm_id() if rank == 0 else None)
+        try:
+            eng = Engine(comm_id=comm, **kw)
+        except Exception as exc:
+            # never measure something else silently: the rank exits non-zero
+            # and the launcher (or launch_ranks) stops the others
+            print(f"bench.py rank {rank}: RCCL exchange unavailable: {exc}", file=sys.stderr)
+            raise SystemExit(3)
+        exchange = "rccl"
     # steady state: budget never reached
     budget = (1 << 62)
     ty = 0
@@ -368,6 +432,7 @@ def main():
                 "initial_pings": args.initial, "mailbox_cap": args.mailbox_cap, "batch": 100,
                 "parallelism": f"actor hash partition x{world} (id % {world})",
                 "exchange": exchange,
+                "ranks_share_gpu": bool(world > 1 and same_gpu()),
             },
             "msgs_per_step": round(delivered / args.steps, 1),
             # global atomics (chunk reservations, one per

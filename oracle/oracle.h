@@ -44,6 +44,8 @@ uint64_t or_splitmix_mix(uint64_t x);
 typedef struct { uint64_t last; } or_polyrand_t;
 void     or_polyrand_create(or_polyrand_t* r, uint64_t seed);
 uint64_t or_polyrand_next(or_polyrand_t* r);
+uint64_t or_gups_update_xor(uint64_t streamers, uint64_t chunk, uint64_t iterate);
+uint64_t or_gups_update_xor_literal(uint64_t streamers, uint64_t chunk, uint64_t iterate);
 
 /* ---- BSP simulator ------------------------------------------------------ */
 /* Mirrors include/gpu_actor.h (same handler tables, behaviour ids, state

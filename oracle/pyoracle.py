@@ -61,6 +61,8 @@ def load():
         "or_rand_int": (u64, [vp, u64]), "or_rand_int_unbiased": (u64, [vp, u64]),
         "or_splitmix_next": (u64, [vp]),
         "or_polyrand_create": (None, [vp, u64]), "or_polyrand_next": (u64, [vp]),
+        "or_gups_update_xor": (u64, [u64, u64, u64]),
+        "or_gups_update_xor_literal": (u64, [u64, u64, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

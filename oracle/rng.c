@@ -128,3 +128,43 @@ void or_polyrand_create(or_polyrand_t* r, uint64_t seed)
       (void)or_polyrand_next(r);
   }
 }
+
+/* XOR of every datum a gups_basic run streams (main.pony:67-68, 93-143):
+ * streamer i is seeded PolyRand(chunk * iterate * i) and produces
+ * chunk * (iterate + 1) values (apply(iterate) down to apply(0)); each value d
+ * does t[d & (size-1)] ^= d at its updater (main.pony:157-161), so the XOR of
+ * the whole table moves by the XOR of all of them. PolyRand's step is linear
+ * over GF(2), so the XOR over streamers of their k-th values is the k-th value
+ * of the XOR of their seeds: one stream of chunk * (iterate + 1) steps. */
+uint64_t or_gups_update_xor(uint64_t streamers, uint64_t chunk, uint64_t iterate)
+{
+  uint64_t x = 0;
+  for(uint64_t i = 0; i < streamers; i++)
+  {
+    or_polyrand_t r;
+    or_polyrand_create(&r, chunk * iterate * i);
+    x ^= r.last;
+  }
+  or_polyrand_t s = { x };
+  uint64_t acc = 0;
+  const uint64_t m = chunk * (iterate + 1);
+  for(uint64_t k = 0; k < m; k++)
+    acc ^= or_polyrand_next(&s);
+  return acc;
+}
+
+/* The same XOR with every stream stepped one value at a time (small sizes:
+ * pins the linearity argument above). */
+uint64_t or_gups_update_xor_literal(uint64_t streamers, uint64_t chunk, uint64_t iterate)
+{
+  uint64_t acc = 0;
+  const uint64_t m = chunk * (iterate + 1);
+  for(uint64_t i = 0; i < streamers; i++)
+  {
+    or_polyrand_t r;
+    or_polyrand_create(&r, chunk * iterate * i);
+    for(uint64_t k = 0; k < m; k++)
+      acc ^= or_polyrand_next(&r);
+  }
+  return acc;
+}

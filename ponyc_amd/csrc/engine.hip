@@ -25,6 +25,7 @@
 #include "engine_dev.h"
 #include "zone_dev.h"
 #include "sparse_dev.h"
+#include "step_entry.h"
 
 using namespace gpa;
 
@@ -212,6 +213,9 @@ struct Engine {
   // wmu guards the thread object (joined or detached by whoever reaps it)
   std::mutex wmu;
   std::thread worker;
+  // progress threads that chained a run from their own completion callback:
+  // they cannot join themselves; gpu_actor_shutdown joins them
+  std::vector<std::thread> detached;
   std::atomic<bool> async_busy{false};   // read without the lock
   std::atomic<bool> async_started{false};  // the progress thread holds mu
   int async_rc = 0;
@@ -259,7 +263,11 @@ struct Engine {
   unsigned long long* d_xrecv = nullptr;   // d_xc + R
   unsigned long long* h_xc = nullptr;      // pinned mirror of d_xc
   unsigned int* d_spill_flag = nullptr;    // spill lists in use on any rank (summed)
-  uint32_t xcap = 0;
+  uint32_t xcap = 0;                       // records per peer segment of xout
+  uint64_t xin_cap = 0;                    // records d_xin (and h_xin) hold
+  XSpillRec* d_xspill = nullptr;           // cross-rank records past xcap
+  unsigned int* d_xspill_n = nullptr;
+  uint32_t xspill_cap = 0;
   std::vector<unsigned long long> h_xcount, h_xrecv;   // host transport
   uint64_t remote_total = 0;
   // host transport (gpu_actor_set_transport)
@@ -349,6 +357,15 @@ inline bool reducible_ht(uint32_t ht)
   return ht == GPU_ACTOR_HT_FANIN_ANALYZER || ht == GPU_ACTOR_HT_GUPS_UPDATER;
 }
 
+const std::vector<StepEntry>& step_entries()
+{
+  static const std::vector<StepEntry> v = {
+    step_entry_any(), step_entry_ring(), step_entry_pinger(), step_entry_pinger_det(),
+    step_entry_fanin_sender(), step_entry_gups_streamer(), step_entry_storm(),
+    step_entry_spreader()};
+  return v;
+}
+
 int upload_types()
 {
   TypeDev td[GPU_ACTOR_MAX_TYPES];
@@ -399,8 +416,12 @@ int upload_types()
   e.halt = g.d_sstat ? &g.d_sstat->halt : nullptr;
   e.skipped = g.d_sstat ? &g.d_sstat->skipped : nullptr;
   e.spill_cap = g.spill_cap;
+  e.xspill = g.d_xspill; e.xspill_n = g.d_xspill_n; e.xspill_cap = g.xspill_cap;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
+  // every k_step code object holds its own copy of the constants
+  for(const StepEntry& se : step_entries())
+    HIPCK(se.upload(td, &e, g.stream));
   return 0;
 }
 
@@ -440,10 +461,13 @@ inline bool spill_pending()
 // they were given, and release the halt (SpillRec, engine_dev.h). Uses the
 // status last read into h_sstat. Nothing is dropped unless a spill list
 // itself overflowed (counted; the run then fails with GPU_ACTOR_EMAILBOX).
+// With n_ranks > 1 every rank calls it together (the decision is summed over
+// ranks: settle_spills, run_locked) and it always clears the spill flag, even
+// with nothing of its own to land, so that every rank's next step runs alike.
 int fixup_spill()
 {
   const Engine::SpillStat st = *g.h_sstat;
-  if(!st.spill_n[0] && !st.spill_n[1] && !st.halt) return 0;
+  if(R() == 1 && !st.spill_n[0] && !st.spill_n[1] && !st.halt) return 0;
   uint32_t n[2], most = 0;
   for(int p = 0; p < 2; ++p)
   {
@@ -629,12 +653,15 @@ int check_sticky()
 
 // Cross-rank exchange after a step (n_ranks > 1), with ONE synchronisation:
 //   device: counts all-to-all, trigger count summed (RCCL), then one pinned
-//   readback of send counts, receive counts, the trigger count and the spill
-//   status; host: grouped ncclSend/ncclRecv of the records over xGMI; device:
-//   k_xinject lands them; the trigger bytes are merged when any actor
-//   triggers muting (or did last time on this parity); a spill flag summed
-//   over ranks (k_spill_flag + allreduce, no readback) lets every rank's next
-//   k_step halt alike when any zone overflowed.
+//   readback of send counts, receive counts, the trigger count, the exchange
+//   spill count and the spill status; host: grow xout / xin if this step
+//   needs more room (exchange_room: records past xcap were kept in the
+//   exchange spill list and are placed now — nothing is dropped, as
+//   messageq.c:31-59 drops nothing), then grouped ncclSend/ncclRecv of the
+//   records over xGMI; device: k_xinject lands them; the trigger bytes are
+//   merged when any actor triggers muting (or did last time on this parity);
+//   a spill flag summed over ranks (k_spill_flag + allreduce, no readback)
+//   lets every rank's next k_step halt alike when any zone overflowed.
 // The host transport (gpu_actor_set_transport) does the same through its
 // callbacks, with the records staged through pinned host memory.
 __global__ void k_spill_flag(unsigned int* flag)
@@ -642,41 +669,165 @@ __global__ void k_spill_flag(unsigned int* flag)
   *flag = c_eng.spill_n[0] + c_eng.spill_n[1];
 }
 
+// This rank's spill status as one number (zone spill lists, halt, and the
+// summed flag of the last exchange): summed over ranks by pend_read, it is
+// the same on every rank, so every rank decides alike whether to fix up.
+__global__ void k_spill_local(unsigned long long* out)
+{
+  *out = (unsigned long long)c_eng.spill_n[0] + c_eng.spill_n[1] + *c_eng.halt +
+         (c_eng.nranks > 1 ? *c_eng.spill_flag : 0u);
+}
+
+// Only when the exchange spill list itself overflowed (records were lost and
+// counted): send what xout holds, and count the kept spill records as lost too.
+__global__ void k_xprep()
+{
+  const unsigned int xs = *c_eng.xspill_n;
+  if(xs <= c_eng.xspill_cap) return;
+  const uint32_t p = threadIdx.x;
+  if(p < c_eng.nranks)
+    c_eng.xcount[p] = min(c_eng.xcount[p], (unsigned long long)c_eng.xcap);
+  if(p == 0) atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], (unsigned long long)c_eng.xspill_cap);
+}
+
+__global__ void __launch_bounds__(kBlock) k_xspill_place(uint32_t n)
+{
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if(i >= n) return;
+  const XSpillRec r = c_eng.xspill[i];
+  c_eng.xout[(size_t)r.peer * c_eng.xcap + r.pos] = r.rec;
+}
+
+int alloc_xspill(uint32_t cap)
+{
+  if(g.d_xspill) HIPCK(hipFree(g.d_xspill));
+  g.d_xspill = nullptr;
+  HIPCK(hipMalloc(&g.d_xspill, (size_t)cap * sizeof(XSpillRec)));
+  g.xspill_cap = cap;
+  return 0;
+}
+
+// Room for this step's exchange: max_send records to one peer, total_recv
+// records from all peers, xs records kept in the exchange spill list. xout's
+// peer segments grow (kept records are copied to the new stride) and the
+// spilled records go to their reserved positions; xin grows. Local decisions
+// only: each side sizes its own buffers.
+int exchange_room(uint64_t max_send, uint64_t total_recv, uint64_t xs)
+{
+  const bool lost = xs > g.xspill_cap;     // k_xprep clipped the counts to xcap
+  if(max_send > g.xcap || lost)
+  {
+    uint64_t cap = std::max<uint64_t>(2ull * g.xcap, max_send + max_send / 2);
+    cap = std::min<uint64_t>((cap + 63) & ~63ull, 0x40000000ull);
+    XRec* nx = nullptr;
+    HIPCK(hipMalloc(&nx, (size_t)R() * cap * sizeof(XRec)));
+    HIPCK(hipMemcpy2DAsync(nx, cap * sizeof(XRec), g.d_xout, (size_t)g.xcap * sizeof(XRec),
+      (size_t)g.xcap * sizeof(XRec), R(), hipMemcpyDeviceToDevice, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    HIPCK(hipFree(g.d_xout));
+    g.d_xout = nx;
+    if(g.xp_a2a)
+    {
+      HIPCK(hipHostFree(g.h_xout));
+      g.h_xout = nullptr;
+      HIPCK(hipHostMalloc(&g.h_xout, (size_t)R() * cap * sizeof(XRec), hipHostMallocDefault));
+    }
+    g.xcap = (uint32_t)cap;
+    const int rc = upload_types();
+    if(rc) return rc;
+  }
+  if(xs)
+  {
+    if(!lost)
+    {
+      hipLaunchKernelGGL(k_xspill_place, dim3(blocks_for(xs)), dim3(kBlock), 0, g.stream,
+        (uint32_t)xs);
+      HIPCK(hipGetLastError());
+    }
+    HIPCK(hipMemsetAsync(g.d_xspill_n, 0, sizeof(unsigned int), g.stream));
+    if(xs > g.xspill_cap / 2)
+    {
+      // a burst this large may come again: keep room for twice as much
+      HIPCK(hipStreamSynchronize(g.stream));
+      const int rc = alloc_xspill((uint32_t)std::min<uint64_t>(4ull * std::max<uint64_t>(xs,
+        g.xspill_cap), 1ull << 27));
+      if(rc) return rc;
+      const int rc2 = upload_types();
+      if(rc2) return rc2;
+    }
+  }
+  if(total_recv > g.xin_cap)
+  {
+    const uint64_t cap = std::max<uint64_t>(2ull * g.xin_cap, total_recv + total_recv / 2);
+    HIPCK(hipStreamSynchronize(g.stream));
+    HIPCK(hipFree(g.d_xin));
+    g.d_xin = nullptr;
+    HIPCK(hipMalloc(&g.d_xin, cap * sizeof(XRec)));
+    if(g.xp_a2a)
+    {
+      HIPCK(hipHostFree(g.h_xin));
+      g.h_xin = nullptr;
+      HIPCK(hipHostMalloc(&g.h_xin, cap * sizeof(XRec), hipHostMallocDefault));
+    }
+    g.xin_cap = cap;
+  }
+  return 0;
+}
+
+// Trigger bytes in use: global ids L * R + r for every local slot L of the
+// largest rank's zones (the same count on every rank, as the merge needs).
+uint64_t trig_live_bytes()
+{
+  const uint64_t per_rank = (g.n_actors + R() - 1) / R();
+  const uint64_t zones = (per_rank + kZone - 1) / kZone;
+  return std::min<uint64_t>(g.trig_bytes, (zones * kZone * R() + 7) & ~7ull);
+}
+
 int exchange_step(uint32_t step_sidx)
 {
   const uint32_t n = R(), land_par = g.par, tslot = (step_sidx + 1) % 3;
   unsigned int tcount = 0;
   uint64_t total = 0;
+  hipLaunchKernelGGL(k_xprep, dim3(1), dim3(64), 0, g.stream);
+  HIPCK(hipGetLastError());
   if(g.xp_a2a)
   {
-    unsigned int tloc = 0;
+    unsigned int tloc = 0, xs = 0;
     HIPCK(hipMemcpyAsync(g.h_xc, g.d_xcount, n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
       g.stream));
     HIPCK(hipMemcpyAsync(&tloc, g.d_trig_n + tslot, sizeof(tloc), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipMemcpyAsync(&xs, g.d_xspill_n, sizeof(xs), hipMemcpyDeviceToHost, g.stream));
     HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
       g.stream));
     HIPCK(hipStreamSynchronize(g.stream));
-    std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n), rc(n, 0);
+    std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n), rcv(n, 0);
+    uint64_t max_send = 0;
     for(uint32_t p = 0; p < n; ++p)
-      sc[p] = p == rank() ? 0 : std::min<unsigned long long>(g.h_xc[p], g.xcap);
-    if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rc.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
+    {
+      sc[p] = p == rank() ? 0 : g.h_xc[p];
+      max_send = std::max(max_send, sc[p]);
+    }
+    if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rcv.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
     uint64_t t64 = tloc;
     if(g.xp_ar(g.xp_ctx, &t64, 1) != 0) return GPU_ACTOR_ECOMM;
     tcount = (unsigned int)t64;
     HIPCK(hipMemcpyAsync(g.d_trig_n + tslot, &tcount, sizeof(tcount), hipMemcpyHostToDevice,
       g.stream));
+    uint64_t rtot = 0;
+    for(uint32_t p = 0; p < n; ++p) rtot += rcv[p];
+    int rc = exchange_room(max_send, rtot, xs);
+    if(rc) return rc;
     uint64_t soff = 0;
     for(uint32_t p = 0; p < n; ++p)
     {
-      rc[p] = std::min<uint64_t>(rc[p], g.xcap);
       if(sc[p])
         HIPCK(hipMemcpyAsync(g.h_xout + soff, g.d_xout + (size_t)p * g.xcap, sc[p] * sizeof(XRec),
           hipMemcpyDeviceToHost, g.stream));
       soff += sc[p];
-      total += rc[p];
+      total += rcv[p];
       sb[p] = sc[p] * sizeof(XRec);
-      rb[p] = rc[p] * sizeof(XRec);
-      g.h_xc[n + p] = rc[p];
+      rb[p] = rcv[p] * sizeof(XRec);
+      g.h_xc[n + p] = rcv[p];
     }
     HIPCK(hipStreamSynchronize(g.stream));
     if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
@@ -691,29 +842,39 @@ int exchange_step(uint32_t step_sidx)
     NCCLCK(ncclAllToAll(g.d_xcount, g.d_xrecv, 1, ncclUint64, g.comm, g.stream));
     NCCLCK(ncclAllReduce(g.d_trig_n + tslot, g.d_trig_n + tslot, 1, ncclUint32, ncclSum, g.comm,
       g.stream));
+    g.h_xc[2 * n] = 0;
+    g.h_xc[2 * n + 1] = 0;
     HIPCK(hipMemcpyAsync(g.h_xc, g.d_xc, 2 * n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
       g.stream));
     HIPCK(hipMemcpyAsync(g.h_xc + 2 * n, g.d_trig_n + tslot, sizeof(unsigned int),
+      hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipMemcpyAsync(g.h_xc + 2 * n + 1, g.d_xspill_n, sizeof(unsigned int),
       hipMemcpyDeviceToHost, g.stream));
     HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
       g.stream));
     HIPCK(hipStreamSynchronize(g.stream));            // the step's one synchronisation
     tcount = (unsigned int)(g.h_xc[2 * n] & 0xFFFFFFFFull);
+    const uint64_t xs = g.h_xc[2 * n + 1] & 0xFFFFFFFFull;
     std::vector<uint64_t> roff(n);
+    uint64_t max_send = 0;
     for(uint32_t p = 0; p < n; ++p)
     {
       roff[p] = total;
-      total += std::min<unsigned long long>(g.h_xc[n + p], g.xcap);
+      if(p == rank()) continue;
+      total += g.h_xc[n + p];
+      max_send = std::max<uint64_t>(max_send, g.h_xc[p]);
     }
+    int rc = exchange_room(max_send, total, xs);
+    if(rc) return rc;
     NCCLCK(ncclGroupStart());
     for(uint32_t p = 0; p < n; ++p)
     {
       if(p == rank()) continue;
-      const uint64_t sc = std::min<unsigned long long>(g.h_xc[p], g.xcap);
-      const uint64_t rc = std::min<unsigned long long>(g.h_xc[n + p], g.xcap);
+      const uint64_t sc = g.h_xc[p];
+      const uint64_t rcn = g.h_xc[n + p];
       if(sc) NCCLCK(ncclSend(g.d_xout + (size_t)p * g.xcap, sc * sizeof(XRec), ncclUint8, p,
         g.comm, g.stream));
-      if(rc) NCCLCK(ncclRecv(g.d_xin + roff[p], rc * sizeof(XRec), ncclUint8, p, g.comm,
+      if(rcn) NCCLCK(ncclRecv(g.d_xin + roff[p], rcn * sizeof(XRec), ncclUint8, p, g.comm,
         g.stream));
     }
     NCCLCK(ncclGroupEnd());
@@ -727,22 +888,23 @@ int exchange_step(uint32_t step_sidx)
   }
   HIPCK(hipMemsetAsync(g.d_xcount, 0, n * sizeof(unsigned long long), g.stream));
   // trigger bytes of parity land_par: every rank's own bytes summed (each
-  // byte has one writer, so the sum is the merge)
+  // byte has one writer, so the sum is the merge), over the ids in use only
   if(tcount || g.trig_stale[land_par])
   {
+    const uint64_t tb = trig_live_bytes();
     if(g.xp_ar)
     {
-      std::vector<uint64_t> h(g.trig_bytes / 8);
-      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[land_par], g.trig_bytes, hipMemcpyDeviceToHost,
+      std::vector<uint64_t> h(tb / 8);
+      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[land_par], tb, hipMemcpyDeviceToHost,
         g.stream));
       HIPCK(hipStreamSynchronize(g.stream));
       if(g.xp_ar(g.xp_ctx, h.data(), h.size()) != 0) return GPU_ACTOR_ECOMM;
-      HIPCK(hipMemcpyAsync(g.d_trig[land_par], h.data(), g.trig_bytes, hipMemcpyHostToDevice,
+      HIPCK(hipMemcpyAsync(g.d_trig[land_par], h.data(), tb, hipMemcpyHostToDevice,
         g.stream));
       HIPCK(hipStreamSynchronize(g.stream));
     }
     else
-      NCCLCK(ncclAllReduce(g.d_trig_own[land_par], g.d_trig[land_par], g.trig_bytes, ncclUint8,
+      NCCLCK(ncclAllReduce(g.d_trig_own[land_par], g.d_trig[land_par], tb, ncclUint8,
         ncclSum, g.comm, g.stream));
   }
   g.trig_stale[land_par] = tcount != 0;
@@ -766,26 +928,25 @@ int exchange_step(uint32_t step_sidx)
 
 // k_step compiled for the one handler table all serial actors share, when
 // they do (smaller code, no spills); the any-mix instantiation otherwise.
-typedef void (*step_kernel_t)(uint32_t, uint32_t, uint32_t);
 step_kernel_t pick_step_kernel()
 {
   int only = -1;
   for(const HostType& t : g.types)
   {
     if(!t.created || reducible_ht(t.ht)) continue;
-    if(only >= 0 && (uint32_t)only != t.ht) return k_step<-1>;
+    if(only >= 0 && (uint32_t)only != t.ht) return step_entry_any().kernel;
     only = (int)t.ht;
   }
   switch(only)
   {
-    case GPU_ACTOR_HT_RING: return k_step<GPU_ACTOR_HT_RING>;
-    case GPU_ACTOR_HT_PINGER: return k_step<GPU_ACTOR_HT_PINGER>;
-    case GPU_ACTOR_HT_PINGER_DET: return k_step<GPU_ACTOR_HT_PINGER_DET>;
-    case GPU_ACTOR_HT_FANIN_SENDER: return k_step<GPU_ACTOR_HT_FANIN_SENDER>;
-    case GPU_ACTOR_HT_GUPS_STREAMER: return k_step<GPU_ACTOR_HT_GUPS_STREAMER>;
-    case GPU_ACTOR_HT_STORM: return k_step<GPU_ACTOR_HT_STORM>;
-    case GPU_ACTOR_HT_SPREADER: return k_step<GPU_ACTOR_HT_SPREADER>;
-    default: return k_step<-1>;
+    case GPU_ACTOR_HT_RING: return step_entry_ring().kernel;
+    case GPU_ACTOR_HT_PINGER: return step_entry_pinger().kernel;
+    case GPU_ACTOR_HT_PINGER_DET: return step_entry_pinger_det().kernel;
+    case GPU_ACTOR_HT_FANIN_SENDER: return step_entry_fanin_sender().kernel;
+    case GPU_ACTOR_HT_GUPS_STREAMER: return step_entry_gups_streamer().kernel;
+    case GPU_ACTOR_HT_STORM: return step_entry_storm().kernel;
+    case GPU_ACTOR_HT_SPREADER: return step_entry_spreader().kernel;
+    default: return step_entry_any().kernel;
   }
 }
 
@@ -829,15 +990,19 @@ int spawn_process(uint32_t cur)
       HIPCK(hipStreamSynchronize(g.stream));
       HIPCK(hipFree(dall));
     }
-    // rank order, clipped to the reserve (the same clip on every rank)
+    // every rank's whole list, in rank order (each list holds at most
+    // spawn_cap records; past that its own device counted the drops): the
+    // reserve is applied per type after the canonical sort (k_spawn_land), so
+    // which spawns get ids never depends on the rank layout
     std::vector<uint64_t> off(nr);
     uint64_t acc = 0;
     for(uint32_t p = 0; p < nr; ++p)
     {
-      cnt[p] = std::min<uint64_t>(cnt[p], g.spawn_cap - acc);
+      cnt[p] = std::min<uint64_t>(cnt[p], g.spawn_cap);
       off[p] = acc;
       acc += cnt[p];
     }
+    if(acc > 0x7FFFFFFFull) return GPU_ACTOR_ERANGE;
     total = (uint32_t)acc;
     if(total == 0) return 0;
     n = (uint32_t)cnt[rank()];
@@ -1063,6 +1228,8 @@ void free_all()
   if(g.d_msgs) (void)hipFree(g.d_msgs);
   if(g.d_xout) (void)hipFree(g.d_xout);
   if(g.d_xin) (void)hipFree(g.d_xin);
+  if(g.d_xspill) (void)hipFree(g.d_xspill);
+  if(g.d_xspill_n) (void)hipFree(g.d_xspill_n);
   if(g.d_xc) (void)hipFree(g.d_xc);
   if(g.h_xc) (void)hipHostFree(g.h_xc);
   if(g.d_spill_flag) (void)hipFree(g.d_spill_flag);
@@ -1236,6 +1403,13 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
     }
     HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
     HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
+    g.xin_cap = (uint64_t)R() * g.xcap;
+    HIPCK(hipMalloc(&g.d_xspill_n, sizeof(unsigned int)));
+    HIPCK(hipMemsetAsync(g.d_xspill_n, 0, sizeof(unsigned int), g.stream));
+    {
+      const int xrc = alloc_xspill(std::max<uint32_t>(1u << 18, g.xcap / 2));
+      if(xrc) return xrc;
+    }
     HIPCK(hipMalloc(&g.d_xc, (2 * R() + 2) * sizeof(unsigned long long)));
     HIPCK(hipMemsetAsync(g.d_xc, 0, (2 * R() + 2) * sizeof(unsigned long long), g.stream));
     HIPCK(hipHostMalloc(&g.h_xc, (2 * R() + 2) * sizeof(unsigned long long), hipHostMallocDefault));
@@ -1263,7 +1437,9 @@ void join_worker()
     if(!g.worker.joinable()) return;
     if(g.worker.get_id() == std::this_thread::get_id())
     {
-      g.worker.detach();
+      // it cannot join itself: gpu_actor_shutdown joins it later, so its
+      // completion callback has returned before anything it runs is freed
+      g.detached.push_back(std::move(g.worker));
       return;
     }
     t = std::move(g.worker);
@@ -1271,9 +1447,28 @@ void join_worker()
   t.join();
 }
 
+// Joins the progress threads that chained runs from their callbacks (all
+// but the calling thread itself); caller must NOT hold g.mu.
+void join_detached()
+{
+  std::vector<std::thread> ts;
+  {
+    std::lock_guard<std::mutex> wl(g.wmu);
+    for(auto& t : g.detached)
+    {
+      if(t.get_id() == std::this_thread::get_id()) t.detach();   // returns after this call
+      else ts.push_back(std::move(t));
+    }
+    g.detached.clear();
+  }
+  for(auto& t : ts)
+    if(t.joinable()) t.join();
+}
+
 GPU_ACTOR_API int gpu_actor_shutdown(void)
 {
   join_worker();                      // an async run finishes first
+  join_detached();
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init) return GPU_ACTOR_ESTATE;
   if(g.stream) (void)hipStreamSynchronize(g.stream);
@@ -1307,6 +1502,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
   g.d_xc = nullptr; g.h_xc = nullptr; g.d_spill_flag = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
+  g.xin_cap = 0; g.d_xspill = nullptr; g.d_xspill_n = nullptr; g.xspill_cap = 0;
   g.h_xout = g.h_xin = nullptr;
   return 0;
 }
@@ -1422,13 +1618,14 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
     // the spawn buffers hold one record per reserved id; nothing is in them
     // between steps, so growing them drops nothing
     HIPCK(hipStreamSynchronize(g.stream));
+    // the gathered list of n_ranks > 1 holds every rank's records
     const uint32_t cap = g.spawn_cap + (uint32_t)t.reserve;
     for(int p = 0; p < 2; ++p)
     {
       if(g.d_skey[p]) HIPCK(hipFree(g.d_skey[p]));
       if(g.d_sarg[p]) HIPCK(hipFree(g.d_sarg[p]));
-      HIPCK(hipMalloc(&g.d_skey[p], (size_t)cap * sizeof(uint64_t)));
-      HIPCK(hipMalloc(&g.d_sarg[p], (size_t)cap * sizeof(uint64_t)));
+      HIPCK(hipMalloc(&g.d_skey[p], (size_t)cap * R() * sizeof(uint64_t)));
+      HIPCK(hipMalloc(&g.d_sarg[p], (size_t)cap * R() * sizeof(uint64_t)));
     }
     g.spawn_cap = cap;
     rc = upload_types();
@@ -1539,6 +1736,29 @@ int pending_now(unsigned long long& out)
   return 0;
 }
 
+// Zone overflow left by the last operation: grow the zones and land the
+// spilled records. One rank decides from its own status. With n_ranks > 1 the
+// decision is this status summed over ranks (k_spill_local + pend_read, a
+// collective every rank makes at the same point), so all ranks run
+// fixup_spill — and clear their spill flags — together or none does.
+int settle_spills()
+{
+  if(R() == 1)
+  {
+    const int rc = read_sstat();
+    if(rc) return rc;
+    return spill_pending() ? fixup_spill() : 0;
+  }
+  hipLaunchKernelGGL(k_spill_local, dim3(1), dim3(1), 0, g.stream, g.d_pend + kPendPre);
+  HIPCK(hipGetLastError());
+  HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+    g.stream));
+  std::vector<unsigned long long> pv;
+  const int rc = pend_read(kPendPre, 1, pv);
+  if(rc) return rc;
+  return pv[0] ? fixup_spill() : 0;
+}
+
 // The scheduler loop to quiescence (or max_steps); caller holds g.mu.
 // One rank: chunks of kChunk k_step launches with one readback each, or
 // k_sparse launches while few records are pending. A zone that overflowed
@@ -1554,9 +1774,7 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
   uint64_t done = 0;
   if(g.n_zones)
   {
-    int rc = read_sstat();
-    if(rc) return rc;
-    rc = fixup_spill();
+    int rc = settle_spills();
     if(rc) return rc;
     unsigned long long before = 0;
     rc = pending_now(before);
@@ -1608,19 +1826,25 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       par_at[k] = g.par;
       rc = launch_pending(k);
       if(rc) return rc;
+      // pend[k + 1]: the spill status, summed over ranks with the counts, so
+      // every rank takes the same branch below (one rank: its own status)
+      hipLaunchKernelGGL(k_spill_local, dim3(1), dim3(1), 0, g.stream, g.d_pend + k + 1);
+      HIPCK(hipGetLastError());
       HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
         g.stream));
-      rc = pend_read(0, k + 1, pv);
+      rc = pend_read(0, k + 2, pv);
       if(rc) return rc;
       uint32_t j = 0;
       bool halted = false;
       for(; j < k && before > 0; ++j)
       {
-        if(pv[j] == kPendSkipped) { halted = true; break; }
+        // one rank: a step the overflow halted; n_ranks > 1 re-runs halted
+        // steps inside launch_step, so no summed slot reads as skipped
+        if(R() == 1 && pv[j] == kPendSkipped) { halted = true; break; }
         ++done;
         before = pv[j + 1];
       }
-      if(halted || spill_pending())
+      if(halted || pv[k + 1] != 0)
       {
         // steps from j on did not run: resume at the parity step j would have read
         if(halted) { g.par = par_at[j]; g.sidx = sidx_at[j]; }
@@ -1723,9 +1947,7 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   // wall step).
   int rc = ensure_events(2);
   if(rc) return rc;
-  rc = read_sstat();
-  if(rc) return rc;
-  rc = fixup_spill();
+  rc = settle_spills();
   if(rc) return rc;
   uint64_t left = n;
   double ms_total = 0.0;
@@ -1740,12 +1962,29 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
       if(rc) return rc;
     }
     HIPCK(hipEventRecord(g.ev[1], g.stream));
-    rc = read_sstat();                      // synchronises the stream
-    if(rc) return rc;
+    bool any;
+    if(R() == 1)
+    {
+      rc = read_sstat();                    // synchronises the stream
+      if(rc) return rc;
+      any = spill_pending();
+    }
+    else
+    {
+      // the same decision on every rank (see settle_spills)
+      hipLaunchKernelGGL(k_spill_local, dim3(1), dim3(1), 0, g.stream, g.d_pend + kPendPre);
+      HIPCK(hipGetLastError());
+      HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+        g.stream));
+      std::vector<unsigned long long> pv;
+      rc = pend_read(kPendPre, 1, pv);       // synchronises the stream
+      if(rc) return rc;
+      any = pv[0] != 0;
+    }
     float ms = 0.f;
     HIPCK(hipEventElapsedTime(&ms, g.ev[0], g.ev[1]));
     ms_total += ms;
-    if(!spill_pending()) break;
+    if(!any) break;
     // steps after an overflow did not run (one rank): grow, then run them
     const uint64_t skipped = std::min<uint64_t>(g.h_sstat->skipped, left);
     const uint64_t ran = left - skipped;

@@ -92,6 +92,16 @@ constexpr unsigned long long kPendSkipped = ~0ull;   // pend[] mark of a step th
 constexpr uint32_t kXSeqApply = 0x3FFFu;
 constexpr uint32_t kXSeqMax = 0x3FFEu;
 static_assert(sizeof(XRec) == 16, "XRec is 16 B");
+// A cross-rank record past its peer segment's capacity (xcap): kept with its
+// peer and reserved position; the host grows xout and places it before the
+// exchange sends anything (messageq.c:31-59 is unbounded; so is the exchange).
+struct XSpillRec {       // 32 B
+  XRec     rec;
+  uint32_t peer;
+  uint32_t pos;
+  uint32_t pad[2];
+};
+static_assert(sizeof(XSpillRec) == 32, "XSpillRec is 32 B");
 
 __device__ __forceinline__ uint64_t zkey(const ZRec& r)
 {
@@ -153,6 +163,10 @@ struct EngDev {
   unsigned int* halt;             // set by a skipped step: every later step skips too
   unsigned long long* skipped;    // steps skipped since the last fixup
   uint32_t spill_cap, pad4;
+  // cross-rank records past xcap (n_ranks > 1): placed by the host after growing xout
+  XSpillRec* xspill;
+  unsigned int* xspill_n;
+  uint32_t xspill_cap, pad5;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -308,6 +322,24 @@ __device__ __forceinline__ void spill_rec(uint32_t p, uint32_t kind, uint32_t z,
     atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);   // the spill list itself is full
 }
 
+// Store cross-rank record x at reserved position pos of peer segment `peer`;
+// past the segment's capacity it goes to the exchange spill list (lost, and
+// counted, only when that list is full too). Returns 1 if it was lost.
+__device__ __forceinline__ uint32_t xout_store(uint32_t peer, uint32_t pos, const XRec& x)
+{
+  if(pos < c_eng.xcap)
+  {
+    c_eng.xout[(size_t)peer * c_eng.xcap + pos] = x;
+    return 0;
+  }
+  const unsigned int i = atomicAdd(c_eng.xspill_n, 1u);
+  if(i >= c_eng.xspill_cap) return 1;
+  uint32_t* d = reinterpret_cast<uint32_t*>(c_eng.xspill + i);
+  *reinterpret_cast<uint4*>(d) = make_uint4(x.w0, x.w1, (uint32_t)x.arg, (uint32_t)(x.arg >> 32));
+  *reinterpret_cast<uint4*>(d + 4) = make_uint4(peer, pos, 0u, 0u);
+  return 0;
+}
+
 // Store landing record v of zone z at reserved position pos of parity p.
 __device__ __forceinline__ void land_store(uint32_t p, uint32_t z, uint32_t pos, const uint4& v)
 {
@@ -338,11 +370,7 @@ __device__ __forceinline__ void send_direct(uint32_t nxt, uint32_t self, uint32_
   else
   {
     const unsigned long long pos = atomicAdd(&c_eng.xcount[b - nz], 1ull);
-    if(pos < c_eng.xcap)
-    {
-      c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] = xpack(to, w, self, arg);
-    }
-    else
+    if(pos > 0x3FFFFFFFull || xout_store(b - nz, (uint32_t)pos, xpack(to, w, self, arg)))
       atomicAdd(&c_eng.stats[ST_XCHG_OVERFLOW], 1ull);
   }
 }

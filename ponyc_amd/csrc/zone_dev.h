@@ -1110,15 +1110,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         spill_rec(nxt, 0u, b, pos, v);
     }
     else
-    {
-      if(pos < c_eng.xcap)
-      {
-        c_eng.xout[(size_t)(b - nz) * c_eng.xcap + pos] =
-          xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z);
-      }
-      else
-        ++xover;
-    }
+      xover += xout_store(b - nz, pos, xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z));
   };
   if(nout <= kZoneThreads)
   {
@@ -1198,6 +1190,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
 }
 
+// The helper kernels below belong to engine.hip's code object only (the
+// step_*.hip units define GPA_STEP_TU and instantiate k_step alone).
+#ifndef GPA_STEP_TU
 // Pending mail (carried + landed) for parity `cur`, summed into pend[slot].
 __global__ void __launch_bounds__(kBlock) k_pending(uint32_t cur, uint32_t slot)
 {
@@ -1219,6 +1214,8 @@ __global__ void __launch_bounds__(kBlock) k_pending(uint32_t cur, uint32_t slot)
     if(tot) atomicAdd(&c_eng.pend[slot], tot);
   }
 }
+
+#endif // GPA_STEP_TU
 
 // Landing of records addressed to this rank's serial actors (host sends,
 // records from other ranks): a block of kLandThreads threads takes
@@ -1267,6 +1264,7 @@ __device__ __forceinline__ void land_records(LandRec (&r)[kLandPer], uint32_t cu
     }
 }
 
+#ifndef GPA_STEP_TU
 // Host sends (pony_sendv from outside the runtime): hseq gives the canonical
 // order; host senders rank above every actor id.
 __global__ void __launch_bounds__(kLandThreads) k_inject(const gpu_msg_t* msgs, uint64_t n,
@@ -1308,8 +1306,8 @@ __global__ void __launch_bounds__(kLandThreads) k_inject(const gpu_msg_t* msgs, 
 }
 
 // Records received from other ranks: `in` holds each peer's records in rank
-// order, rcnt[p] of them from peer p (clipped to xcap); the sender's rank of a
-// record is the segment it lies in.
+// order, rcnt[p] of them from peer p; the sender's rank of a record is the
+// segment it lies in.
 __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64_t n, uint32_t cur,
   const unsigned long long* rcnt)
 {
@@ -1325,7 +1323,7 @@ __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64
     for(uint32_t p = 0; p < R; ++p)
     {
       s_roff[p] = acc;
-      acc += min(rcnt[p], (unsigned long long)c_eng.xcap);
+      acc += rcnt[p];
     }
   }
   __syncthreads();
@@ -1368,5 +1366,6 @@ __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64
     atomicAdd(&c_eng.stats[ST_BY_TYPE + threadIdx.x], s_app[threadIdx.x]);
   }
 }
+#endif // GPA_STEP_TU
 
 } // namespace gpa

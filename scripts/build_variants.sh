@@ -1,9 +1,14 @@
-# Build A/B variants of the engine (compile-time toggles) into ponyc_amd/variants/.
+# Build A/B variants of the engine (compile-time toggles) into ponyc_amd/variants/
+# (objects under ponyc_amd/build/lib_<name>/; the units build in parallel).
 set -e
 cd "$(dirname "$0")/.."
 OUT=ponyc_amd/variants
 mkdir -p $OUT
-b() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" -o $OUT/lib_$name.so ponyc_amd/csrc/engine.hip -lrccl & }
+b() {
+  name=$1; shift
+  python3 -c "import sys; from ponyc_amd import build as b; b.build(defines=sys.argv[2:], out=sys.argv[1])" \
+    $OUT/lib_$name.so "$@"
+}
 for v in "$@"; do
   case $v in
     base) b base ;;
@@ -12,5 +17,4 @@ for v in "$@"; do
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
-wait
 ls -la $OUT

@@ -41,7 +41,37 @@ CASES = {
     # zone overflow on one rank halts the next step on every rank until grown
     "spill": (lambda e: W.fifo(e, 300, 3, 4, 9, batch=4, mailbox_cap=1), W.fifo_result,
               {"mailbox_cap": 1}),
+    # one sink (rank 0 only): its zone overflows on rank 0 alone, in the last
+    # step of a run — run one step at a time, and run_fixed one step at a time
+    "spill_one_rank": (lambda e: W.fifo(e, 300, 1, 4, 9, batch=4, mailbox_cap=1), W.fifo_result,
+                       {"mailbox_cap": 1}, "steps"),
+    "spill_one_rank_fixed": (lambda e: W.fifo(e, 300, 1, 4, 9, batch=4, mailbox_cap=1),
+                             W.fifo_result, {"mailbox_cap": 1}, "fixed"),
+    # 64 cross-rank records per peer segment against ~8K per step: the
+    # exchange keeps the rest in its spill list, grows, and drops nothing
+    "xspill": (lambda e: W.ubench(e, 4096, 4, 32), W.ubench_result, {"max_exchange": 64}),
+    "xspill_det": (lambda e: W.ubench(e, 3001, 3, det=True, hops=40), W.ubench_result,
+                   {"max_exchange": 16}, "steps"),
 }
+
+
+def drive(eng, mode: str) -> int:
+    """run to quiescence: in one call, one step per call, or run_fixed(1) steps"""
+    if mode == "run":
+        return eng.run(0)
+    steps = 0
+    while True:
+        if mode == "steps":
+            k = eng.run(1)
+        else:
+            if eng.counts()["pending"] == 0:
+                break
+            eng.run_fixed(1)
+            k = 1
+        if k == 0:
+            break
+        steps += k
+    return steps
 
 
 def main():
@@ -53,7 +83,8 @@ def main():
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    setup, result, kw = CASES[a.case]
+    setup, result, kw, *mode = CASES[a.case]
+    mode = mode[0] if mode else "run"
     if a.rccl:
         from ponyc_amd.dist import share_comm_id
         lr = 0 if a.same_gpu else int(os.environ.get("LOCAL_RANK", rank))
@@ -61,7 +92,7 @@ def main():
     else:
         eng = Engine(device=0, n_ranks=world, rank=rank, transport=GlooTransport(), **kw)
     w = setup(eng)
-    steps = eng.run(0)
+    steps = drive(eng, mode)
     c = eng.counts()
     res = result(GlobalView(eng), w)
     eng.shutdown()

@@ -74,15 +74,51 @@ def test_c4_gups_2p20(engine_factory, oracle):
                     W.gups_result)
 
 
-def test_c5_storm_8m(engine_factory):
-    """C5, one GPU's share: 8M actors, a token ring plus 4 random-target pings
-    per actor, 4 hops each. Conservation and an XOR checksum of every payload."""
-    n, r, hops = 8 * MILLION, 4, 4
+def _xor_upto(n: int) -> int:
+    """0 ^ 1 ^ ... ^ (n - 1)"""
+    m = n - 1
+    return [m, 1, m + 1, 0][m % 4] if n > 0 else 0
+
+
+def test_c4_gups_2p30_2p32(engine_factory):
+    """C4 at its stated size: a 2^30-entry u64 table (8 GiB) as
+    8 updater shards, 2^32 PolyRand updates t[d & (size-1)] ^= d
+    (gups_basic/main.pony:93-216), here 2^18 streamers x 4096 x (3 + 1). The
+    whole table's XOR must equal the initial table's XOR (table[k] = k +
+    index*size, main.pony:145-155) ^ the XOR of every datum streamed, which
+    the oracle's PolyRand restatement computes on the CPU
+    (oracle/rng.c or_gups_update_xor, pinned to the literal stream walk and
+    to a BSP run in tests/test_oracle_golden.py)."""
+    import pyoracle
+    logtable, updaters, streamers, chunk, iterate = 30, 8, 1 << 18, 4096, 3
     e = engine_factory()
-    w = W.storm(e, n, r, hops)
-    e.run()
+    w = W.gups(e, logtable, updaters, streamers, chunk, iterate)
+    assert w["updates"] == 1 << 32
+    steps = e.run()
     c = e.counts()
     assert c["dropped"] == 0 and c["pending"] == 0
+    assert steps == iterate + 1
+    assert c["delivered_by_type"][w["up_type"]] == 1 << 32
+    assert c["delivered_by_type"][w["str_type"]] == streamers * (iterate + 1)
+    table_xor = 0
+    for u in range(updaters):                 # one 1 GiB shard at a time
+        table_xor ^= int(np.bitwise_xor.reduce(e.state_read(w["up_type"], u, 1).reshape(-1)))
+    want = _xor_upto(1 << logtable) ^ pyoracle.load().or_gups_update_xor(streamers, chunk, iterate)
+    assert table_xor == want
+
+
+@pytest.mark.parametrize("hops", [4, 1000])
+def test_c5_storm_8m(engine_factory, hops):
+    """C5, one GPU's share: 8M actors, a token ring plus 4 random-target pings
+    per actor, `hops` hops each (1000: the stated 1000 steps, 41.9 G
+    messages). Conservation and an XOR checksum of every payload."""
+    n, r = 8 * MILLION, 4
+    e = engine_factory()
+    w = W.storm(e, n, r, hops)
+    steps = e.run()
+    c = e.counts()
+    assert c["dropped"] == 0 and c["pending"] == 0
+    assert steps == hops + 1
     total = n * (r + 1) * (hops + 1)
     assert c["delivered"] == total
     st = e.state_read(w["type"])          # [count, acc]

@@ -40,7 +40,8 @@ def test_host_plumbing_gloo(nproc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["ring", "ring1", "ubench", "ubench_det", "fanin", "gups",
                                   "storm", "fifo", "fifo_seq", "spreader", "mute", "priority",
-                                  "spill"])
+                                  "spill", "spill_one_rank", "spill_one_rank_fixed", "xspill",
+                                  "xspill_det"])
 def test_two_ranks_one_gpu(case):
     out = _launch("mr_worker.py", 2, case)
     line = [l for l in out.splitlines() if l.startswith("MR_RESULT ")]

@@ -97,3 +97,27 @@ def test_message_totals_match_reference():
             assert c["delivered"] == msgs + MANIFEST[name]["args"]["count"]
         else:
             assert c["delivered"] == msgs, name
+
+
+def _xor_upto(n: int) -> int:
+    m = n - 1
+    return [m, 1, m + 1, 0][m % 4] if n > 0 else 0
+
+
+def test_gups_update_xor_matches_reference_table():
+    """The C4 full-size check's expected checksum (or_gups_update_xor: the XOR
+    of every datum streamed, by PolyRand's linearity over GF(2)) equals the
+    literal walk of every stream, and moves the table the reference runtime
+    itself produced from its initial XOR (golden gups fixture)."""
+    L = pyoracle.load()
+    assert L.or_gups_update_xor(64, 64, 3) == L.or_gups_update_xor_literal(64, 64, 3)
+    assert L.or_gups_update_xor(5, 100, 7) == L.or_gups_update_xor_literal(5, 100, 7)
+    for name, spec in MANIFEST.items():
+        if spec["harness"] != "gups":
+            continue
+        a = spec["args"]
+        table = expected(name)
+        got = int(np.bitwise_xor.reduce(table.reshape(-1)))
+        want = _xor_upto(1 << a["logtable"]) ^ L.or_gups_update_xor(a["streamers"], a["chunk"],
+                                                                      a["iterate"])
+        assert got == want, name
