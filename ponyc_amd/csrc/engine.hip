@@ -928,25 +928,25 @@ int exchange_step(uint32_t step_sidx)
 
 // k_step compiled for the one handler table all serial actors share, when
 // they do (smaller code, no spills); the any-mix instantiation otherwise.
-step_kernel_t pick_step_kernel()
+StepEntry pick_step_entry()
 {
   int only = -1;
   for(const HostType& t : g.types)
   {
     if(!t.created || reducible_ht(t.ht)) continue;
-    if(only >= 0 && (uint32_t)only != t.ht) return step_entry_any().kernel;
+    if(only >= 0 && (uint32_t)only != t.ht) return step_entry_any();
     only = (int)t.ht;
   }
   switch(only)
   {
-    case GPU_ACTOR_HT_RING: return step_entry_ring().kernel;
-    case GPU_ACTOR_HT_PINGER: return step_entry_pinger().kernel;
-    case GPU_ACTOR_HT_PINGER_DET: return step_entry_pinger_det().kernel;
-    case GPU_ACTOR_HT_FANIN_SENDER: return step_entry_fanin_sender().kernel;
-    case GPU_ACTOR_HT_GUPS_STREAMER: return step_entry_gups_streamer().kernel;
-    case GPU_ACTOR_HT_STORM: return step_entry_storm().kernel;
-    case GPU_ACTOR_HT_SPREADER: return step_entry_spreader().kernel;
-    default: return step_entry_any().kernel;
+    case GPU_ACTOR_HT_RING: return step_entry_ring();
+    case GPU_ACTOR_HT_PINGER: return step_entry_pinger();
+    case GPU_ACTOR_HT_PINGER_DET: return step_entry_pinger_det();
+    case GPU_ACTOR_HT_FANIN_SENDER: return step_entry_fanin_sender();
+    case GPU_ACTOR_HT_GUPS_STREAMER: return step_entry_gups_streamer();
+    case GPU_ACTOR_HT_STORM: return step_entry_storm();
+    case GPU_ACTOR_HT_SPREADER: return step_entry_spreader();
+    default: return step_entry_any();
   }
 }
 
@@ -1107,7 +1107,9 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
   const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
                                                           kSortWork);
-  step_kernel_t kern = pick_step_kernel();
+  const StepEntry se = pick_step_entry();
+  if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
+  step_kernel_t kern = se.kernel;
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
@@ -2028,9 +2030,15 @@ GPU_ACTOR_API int gpu_actor_state_read(uint32_t type_id, uint64_t first, uint64_
   HostType& t = g.types[type_id];
   if(!t.created || first + n > t.lcount) return GPU_ACTOR_EINVAL;
   if(n == 0) return 0;
-  for(uint32_t w = 0; w < t.words; ++w)
-    HIPCK(hipMemcpyAsync(out + (size_t)w * n, t.d_state + (size_t)w * t.lcount + first,
-      n * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
+  // field-major [words][lcount] to [words][n]: one copy (a table type has
+  // millions of words and few actors; a copy per word would take minutes)
+  if(n == t.lcount)
+    HIPCK(hipMemcpyAsync(out, t.d_state, (size_t)t.words * n * sizeof(uint64_t),
+      hipMemcpyDeviceToHost, g.stream));
+  else
+    HIPCK(hipMemcpy2DAsync(out, n * sizeof(uint64_t), t.d_state + first,
+      (size_t)t.lcount * sizeof(uint64_t), n * sizeof(uint64_t), t.words, hipMemcpyDeviceToHost,
+      g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   return 0;
 }
@@ -2048,9 +2056,12 @@ GPU_ACTOR_API int gpu_actor_state_write(uint32_t type_id, uint64_t first, uint64
   HostType& t = g.types[type_id];
   if(!t.created || first + n > t.lcount) return GPU_ACTOR_EINVAL;
   if(n == 0) return 0;
-  for(uint32_t w = 0; w < t.words; ++w)
-    HIPCK(hipMemcpyAsync(t.d_state + (size_t)w * t.lcount + first, in + (size_t)w * n,
-      n * sizeof(uint64_t), hipMemcpyHostToDevice, g.stream));
+  if(n == t.lcount)
+    HIPCK(hipMemcpyAsync(t.d_state, in, (size_t)t.words * n * sizeof(uint64_t),
+      hipMemcpyHostToDevice, g.stream));
+  else
+    HIPCK(hipMemcpy2DAsync(t.d_state + first, (size_t)t.lcount * sizeof(uint64_t), in,
+      n * sizeof(uint64_t), n * sizeof(uint64_t), t.words, hipMemcpyHostToDevice, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   return 0;
 }

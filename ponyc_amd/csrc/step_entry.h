@@ -14,6 +14,7 @@ typedef void (*step_kernel_t)(uint32_t, uint32_t, uint32_t);
 struct StepEntry {
   step_kernel_t kernel;
   hipError_t (*upload)(const TypeDev* types, const EngDev* eng, hipStream_t s);
+  bool stub;               // not compiled in this (experiment) build
 };
 
 StepEntry step_entry_any();             // any mix of handler tables

@@ -7,7 +7,16 @@
 
 namespace gpa {
 
+// A/B experiment builds (-DGPA_STEP_ONLY=<table>) compile one instantiation;
+// the others become stubs the host refuses to launch (GPU_ACTOR_EINVAL).
+#if defined(GPA_STEP_ONLY) && (GPA_STEP_ONLY != GPA_STEP_HT)
+#define GPA_STEP_STUB 1
+template <int HT> __global__ void k_step_stub(uint32_t, uint32_t, uint32_t) {}
+template __global__ void k_step_stub<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
+#else
+#define GPA_STEP_STUB 0
 template __global__ void k_step<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
+#endif
 
 namespace {
 hipError_t step_upload(const TypeDev* types, const EngDev* eng, hipStream_t s)
@@ -19,6 +28,10 @@ hipError_t step_upload(const TypeDev* types, const EngDev* eng, hipStream_t s)
 }
 } // namespace
 
-StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload }; }
+#if GPA_STEP_STUB
+StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true }; }
+#else
+StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload, false }; }
+#endif
 
 } // namespace gpa

@@ -772,13 +772,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
   ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
-  for(uint32_t i = tid; i < nc; i += kZoneThreads)
-  {
-    const ZRec r = C[i];
-    const uint32_t a = r.w0 & kZoneMask;
-    if(use_idx) s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
-    else Sz[s_off[a] + (i - s_aux[a])] = r;
-  }
+  // (the two forms apart: a record held across the branch went to scratch)
+  if(use_idx)
+    for(uint32_t i = tid; i < nc; i += kZoneThreads)
+    {
+      const uint32_t a = C[i].w0 & kZoneMask;
+      s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
+    }
+  else
+    for(uint32_t i = tid; i < nc; i += kZoneThreads)
+    {
+      const uint4 r = *reinterpret_cast<const uint4*>(C + i);
+      const uint32_t a = r.x & kZoneMask;
+      *reinterpret_cast<uint4*>(Sz + s_off[a] + (i - s_aux[a])) = r;
+    }
   if(use_idx)
   {
     // LDS index only: records stay in the landing buffer
@@ -799,12 +806,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     {
       uint4 r[kUnroll];
       uint32_t pos[kUnroll];
+      // unconditional (clamped) loads: all in flight, the records in registers
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
       {
         const uint32_t i = base + u * kZoneThreads + tid;
-        if(i < nl) r[u] = *reinterpret_cast<const uint4*>(Ld + i);
-        else r[u].x = 0xFFFFFFFFu;
+        r[u] = *reinterpret_cast<const uint4*>(Ld + min(i, nl - 1));
+        if(i >= nl) r[u].x = 0xFFFFFFFFu;
       }
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
@@ -1130,11 +1138,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     const uint32_t m = min(kTile, nout - t0);
     uint4 ov[kTilePer];
     uint32_t bk[kTilePer], rk[kTilePer];
+    // every lane loads (past the tile's end: its last record, unused), so the
+    // kTilePer loads are all in flight at once and the tile stays in registers
 #pragma unroll
     for(int u = 0; u < kTilePer; ++u)
     {
-      const uint32_t i = u * kZoneThreads + tid;
-      if(i < m) ov[u] = ld16(reinterpret_cast<const uint4*>(Oz + t0 + i));
+      const uint32_t i = min(u * kZoneThreads + tid, m - 1);
+      ov[u] = ld16(reinterpret_cast<const uint4*>(Oz + t0 + i));
     }
 #pragma unroll
     for(int u = 0; u < kTilePer; ++u)

@@ -6,8 +6,9 @@ to quiescence with gpu_actor_run; rate = delivered messages / wall time of the
 run (host sends done before the clock starts). One JSON line per config.
 With --cpu, the reference runtime (oracle/_ref/harness_*, libponyrt built
 from the reference sources) runs the same config on the host's cores
-(--ponymaxthreads=min(16, cores) --ponynoblock --ponynoscale) and its rate is
-reported beside the GPU's ("cpu_ref").
+(--ponymaxthreads = every usable physical core, bench.py's host_cores rule,
+--ponynoblock --ponynoscale) and its rate is reported beside the GPU's
+("cpu_ref").
 usage: python scripts/bench_configs.py [--cpu] [names...]
 """
 import json
@@ -39,8 +40,13 @@ CONFIGS = {
     # --iterate 8: 151M updates. Ceiling for the access pattern: random 64-bit
     # atomicXor over 2^30 words, 17.75 G/s (scripts/ubench_gups.hip)
     "c4_gups_wide": (lambda e: W.gups(e, 30, 8, 1 << 20, 16, 8), {}),
+    # C4 at its stated size: 2^30-word table as 8 shards, 2^32 updates
+    # (2^18 streamers x 4096 x (3 + 1)); checked in tests/test_gpu_fullsize.py
+    "c4_gups_2p32": (lambda e: W.gups(e, 30, 8, 1 << 18, 4096, 3), {}),
     # C5, one GPU's share: 8M actors, token ring + 4 random pings each, 16 hops
     "c5_storm_8m": (lambda e: W.storm(e, 8 * M, 4, 16), {}),
+    # C5 at its stated 1000 steps (41.9 G messages)
+    "c5_storm_8m_1000": (lambda e: W.storm(e, 8 * M, 4, 1000), {}),
 }
 
 
@@ -60,7 +66,8 @@ def cpu_ref(name):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     harness, args = CPU_REF[name]
-    threads = max(1, min(16, os.cpu_count() or 1))
+    from bench import host_cores             # physical cores ∩ affinity ∩ cgroup quota
+    threads = host_cores()["usable"]
     try:
         info, _ = pyoracle.run_harness(harness, dict(args, threads=threads, noscale=1), None,
                                        timeout=120)
@@ -73,7 +80,8 @@ def cpu_ref(name):
 def main():
     args = sys.argv[1:]
     with_cpu = "--cpu" in args
-    names = [a for a in args if a != "--cpu"] or list(CONFIGS)
+    names = [a for a in args if a != "--cpu"] or [n for n in CONFIGS if not n.endswith("_1000")
+                                                   and n != "c4_gups_2p32"]
     for name in names:
         setup, kw = CONFIGS[name]
         e = Engine(**kw)
