@@ -316,13 +316,6 @@ struct Engine {
   SparseCtl* d_ctl = nullptr;
   SparseCtl* h_ctl = nullptr;             // pinned
   uint64_t sparse_launches = 0, sparse_steps = 0;
-  // planned sends (k_step): per zone its last step's sends per local
-  // destination zone [n_zones][n_zones], whether that plan is in use, and the
-  // hole count of each landing parity
-  uint16_t* d_plan = nullptr;
-  uint32_t* d_plan_on = nullptr;
-  uint32_t plan_nz = 0;
-  unsigned int* d_hole_n = nullptr;
 };
 
 Engine g;
@@ -424,7 +417,6 @@ int upload_types()
   e.skipped = g.d_sstat ? &g.d_sstat->skipped : nullptr;
   e.spill_cap = g.spill_cap;
   e.xspill = g.d_xspill; e.xspill_n = g.d_xspill_n; e.xspill_cap = g.xspill_cap;
-  e.plan = g.d_plan; e.plan_on = g.d_plan_on; e.hole_n = g.d_hole_n;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -563,8 +555,6 @@ int relayout_zones()
     off[z] = total;
     total += (cap[z] + 15u) & ~15u;          // keep every zone 256-B aligned
   }
-  // chunk offsets of planned sends are u32 record offsets (zone_dev.h)
-  if(total >= (1ull << 32)) return GPU_ACTOR_ENOMEM;
   const size_t bytes = std::max<uint64_t>(total, 16) * sizeof(ZRec);
   uint64_t* d_off = nullptr;
   uint32_t* d_cap = nullptr;
@@ -610,17 +600,6 @@ int relayout_zones()
   g.d_zoff = d_off;
   g.d_zcap = d_cap;
   g.zone_records = total;
-  // send plans: a fresh start (they are hints; the zones rebuild them)
-  if(nz != g.plan_nz || !g.d_plan)
-  {
-    if(g.d_plan) HIPCK(hipFree(g.d_plan));
-    if(g.d_plan_on) HIPCK(hipFree(g.d_plan_on));
-    g.d_plan = nullptr; g.d_plan_on = nullptr;
-    HIPCK(hipMalloc(&g.d_plan, std::max<size_t>((size_t)nz * nz, 1) * sizeof(uint16_t)));
-    HIPCK(hipMalloc(&g.d_plan_on, std::max<size_t>(nz, 1) * sizeof(uint32_t)));
-    g.plan_nz = nz;
-  }
-  HIPCK(hipMemsetAsync(g.d_plan_on, 0, std::max<size_t>(nz, 1) * sizeof(uint32_t), g.stream));
   g.n_zones = nz;
   g.zcap_host = cap;
   // the receiver each muted actor waits on, one word per local slot
@@ -1247,9 +1226,6 @@ void free_all()
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
   if(g.d_dbg) (void)hipFree(g.d_dbg);
-  if(g.d_plan) (void)hipFree(g.d_plan);
-  if(g.d_plan_on) (void)hipFree(g.d_plan_on);
-  if(g.d_hole_n) (void)hipFree(g.d_hole_n);
   if(g.h_msgs) (void)hipHostFree(g.h_msgs);
   if(g.d_msgs) (void)hipFree(g.d_msgs);
   if(g.d_xout) (void)hipFree(g.d_xout);
@@ -1389,8 +1365,6 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipHostMalloc(&g.h_sstat, sizeof(Engine::SpillStat), hipHostMallocDefault));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   HIPCK(hipMalloc(&g.d_need, kMaxZones * sizeof(uint32_t)));
-  HIPCK(hipMalloc(&g.d_hole_n, 2 * sizeof(unsigned int)));
-  HIPCK(hipMemsetAsync(g.d_hole_n, 0, 2 * sizeof(unsigned int), g.stream));
   g.trig_bytes = (g.cfg.max_actors + 2 * kZone + 7) & ~7ull;
   for(int p = 0; p < 2; ++p)
   {
@@ -1511,7 +1485,6 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   }
   g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
-  g.d_plan = nullptr; g.d_plan_on = nullptr; g.plan_nz = 0; g.d_hole_n = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
   g.d_spill[0] = g.d_spill[1] = nullptr; g.spill_cap = 0; g.d_sstat = nullptr; g.h_sstat = nullptr;

@@ -42,7 +42,6 @@ constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above ever
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
 constexpr uint32_t kSeqApply = 0xFFFFu;          // outbox marker: reducible apply
 constexpr uint32_t kFanLds = 256;                // analyzers a zone accumulates in LDS
-constexpr uint32_t kHole = 0xFFFFFFFFu;          // w0 of a reserved landing slot no record filled
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
@@ -168,13 +167,6 @@ struct EngDev {
   XSpillRec* xspill;
   unsigned int* xspill_n;
   uint32_t xspill_cap, pad5;
-  // planned sends (zone_dev.h, k_step phase 3): plan[z * n_zones + b] = the
-  // records zone z sent to local zone b in the last step it ran (u16,
-  // saturating), plan_on[z] = some entry is worth a reservation; hole_n[p] =
-  // reserved landing slots of parity p that no record filled (sentinels)
-  uint16_t* plan;
-  uint32_t* plan_on;
-  unsigned int* hole_n;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -284,15 +276,7 @@ struct ZoneCtx : ActorBase {
   uint32_t  ocap;        // its capacity
   uint32_t  nxt;         // landing parity of this step's sends
   uint32_t* s_nout;      // LDS outbox counter
-  uint32_t* s_hist;      // LDS histogram by bucket (records that go through the outbox)
-  // planned sends: per local destination zone b, s_cur[b] counts this step's
-  // sends; the first s_lim[b] of them are stored straight into the chunk the
-  // zone reserved at record offset s_pb[b] of land[nxt] (zone_dev.h)
-  uint32_t* s_cur;
-  const uint32_t* s_lim;
-  const uint32_t* s_pb;
-  ZRec*     land_nxt;
-  uint32_t  n_zones;
+  uint32_t* s_hist;      // LDS histogram by bucket
   __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg) { outbox_put(*this, to, w, arg); }
 };
 // ---- delivery --------------------------------------------------------------
@@ -391,27 +375,9 @@ __device__ __forceinline__ void send_direct(uint32_t nxt, uint32_t self, uint32_
   }
 }
 
-// A send from a zone: into the chunk the zone reserved for the destination
-// zone when there is room left (a planned send: stored once, where the
-// receiver reads it), else parked in the zone outbox and counted in its
-// destination bucket for the scatter.
+// Park one record in the zone outbox and count it in its destination bucket.
 __device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, uint64_t arg)
 {
-  const uint32_t b = bucket_of(to);
-  if(b < a.n_zones)
-  {
-    const uint32_t k = atomicAdd(&a.s_cur[b], 1u);
-    if(k < a.s_lim[b])
-    {
-      uint4 v;
-      v.x = w | (rdiv(to) & kZoneMask);
-      v.y = a.self;
-      v.z = (uint32_t)arg;
-      v.w = (uint32_t)(arg >> 32);
-      *reinterpret_cast<uint4*>(a.land_nxt + a.s_pb[b] + k) = v;
-      return;
-    }
-  }
   const uint32_t idx = atomicAdd(a.s_nout, 1u);
   if(idx >= a.ocap)
   {
@@ -421,7 +387,7 @@ __device__ __forceinline__ void outbox_put(ZoneCtx& a, uint32_t to, uint32_t w, 
   ORec r;
   r.to = to; r.w = w | a.src_local; r.arg = arg;
   *reinterpret_cast<uint4*>(a.out + idx) = *reinterpret_cast<const uint4*>(&r);
-  atomicAdd(&a.s_hist[b], 1u);
+  atomicAdd(&a.s_hist[bucket_of(to)], 1u);
 }
 
 // A handler's send: stamped with its canonical (sender, seq) key now.

@@ -235,30 +235,16 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     }
     return;
   }
+  for(uint32_t i = tid; i < total; i += kSpThreads)
   {
-    // one landing slot per thread (total <= kSpCap <= kSpThreads); holes
-    // (planned chunks' unfilled slots) are left out of the list
-    const uint32_t i = tid;
-    uint4 v = make_uint4(kHole, 0u, 0u, 0u);
-    uint32_t lo = 0;
-    if(i < total)
-    {
-      uint32_t hi = nz;                // zone z with s_zpre[z] <= i < s_zpre[z + 1]
-      while(hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if(s_zpre[m] <= i) lo = m; else hi = m; }
-      v = *reinterpret_cast<const uint4*>(c_eng.land[cur] + c_eng.zoff[lo] + (i - s_zpre[lo]));
-    }
-    const uint32_t keep = v.x != kHole ? 1u : 0u;
-    const uint32_t j = sp_block_excl_scan(keep, s_tmp, total);
-    if(keep)
-    {
-      bK[0][j] = ((uint64_t)(lo * kZone + (v.x & kZoneMask)) << 32) | v.y;
-      bW[0][j] = v.x & ~kZoneMask;
-      bA[0][j] = ((uint64_t)v.w << 32) | v.z;
-    }
+    uint32_t lo = 0, hi = nz;          // zone z with s_zpre[z] <= i < s_zpre[z + 1]
+    while(hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if(s_zpre[m] <= i) lo = m; else hi = m; }
+    const uint4 v = *reinterpret_cast<const uint4*>(c_eng.land[cur] + c_eng.zoff[lo] + (i - s_zpre[lo]));
+    bK[0][i] = ((uint64_t)(lo * kZone + (v.x & kZoneMask)) << 32) | v.y;
+    bW[0][i] = v.x & ~kZoneMask;
+    bA[0][i] = ((uint64_t)v.w << 32) | v.z;
   }
-  // (the zones' send plans describe dense steps: they start over after these)
-  for(uint32_t z = z0; z < z1; ++z) { c_eng.land_n[cur][z] = 0; c_eng.plan_on[z] = 0u; }
-  if(tid == 0) c_eng.hole_n[cur] = 0u;
+  for(uint32_t z = z0; z < z1; ++z) c_eng.land_n[cur][z] = 0;
   // no actor triggers muting now; bytes a zone left in the other parity two
   // steps ago are cleared, so both parities read as all-quiet when the zone
   // path resumes

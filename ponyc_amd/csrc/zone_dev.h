@@ -44,23 +44,6 @@ constexpr int kUnroll = 8;   // independent records in flight per thread in stre
 #ifndef GPA_TILE
 #define GPA_TILE 4096
 #endif
-// Planned sends (phase 3): a zone reserves, before its behaviours run, one
-// chunk per local destination zone it sent at least kPlanMin records to in the
-// last step it ran — that many records plus kPlanSlack — and its handlers store
-// those sends straight into the chunk; the rest go through the outbox and the
-// scatter as before. Unfilled slots become sentinels (w0 = 0xFFFFFFFF, which
-// every reader skips) and are counted in hole_n.
-#ifndef GPA_PLAN
-#define GPA_PLAN 1
-#endif
-#ifndef GPA_PLAN_MIN
-#define GPA_PLAN_MIN 8
-#endif
-#ifndef GPA_PLAN_SLACK
-#define GPA_PLAN_SLACK 2
-#endif
-constexpr uint32_t kPlanMin = GPA_PLAN_MIN;
-constexpr int kPlanSlack = GPA_PLAN_SLACK;   // may be negative: under-reserve
 constexpr uint32_t kIdxCap = GPA_IDX_CAP;  // LDS index budget per zone (records per step)
 constexpr uint32_t kTile = GPA_TILE;       // outbox records sorted per scatter tile (64 KB of LDS)
 constexpr int kTilePer = kTile / kZoneThreads;  // tile records per thread
@@ -648,7 +631,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_red3[3];
   __shared__ uint32_t s_big[kMaxBig];
   __shared__ uint32_t s_nbig;
-  __shared__ uint32_t s_holes;
   constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
@@ -675,9 +657,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   if constexpr(kFan)
     for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
   const uint32_t nxt = cur ^ 1u;
-  // the holes of parity cur are consumed by this step (no one adds to them
-  // before the next step that writes parity cur)
-  if(z == 0 && tid == 0) c_eng.hole_n[cur] = 0u;
   const uint32_t L0 = z * kZone;
   const uint32_t nact = min(kZone, c_eng.n_local - L0);
   const uint32_t R = c_eng.nranks, me = c_eng.rank;
@@ -699,7 +678,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
   for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
-  if(tid == 0) { s_nout = 0; s_ntrig = 0; s_holes = 0; }
+  if(tid == 0) { s_nout = 0; s_ntrig = 0; }
   __syncthreads();
   GPA_STAMP(0);
 
@@ -711,8 +690,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     // an idle zone (uniform: every thread read the same counters) has
     // nothing to count, run or send — the quiet tail of a run, or zones of
     // a sparse workload; it only clears trigger bytes it left two steps ago
-    // (and its plan: it sent nothing this step)
-    if(tid == 0) { c_eng.carry_n[nxt][z] = 0; c_eng.plan_on[z] = 0u; }
+    if(tid == 0) c_eng.carry_n[nxt][z] = 0;
     if(ztn)
     {
       for(uint32_t i = tid; i < nact; i += kZoneThreads) tb_out[(L0 + i) * R + me] = 0;
@@ -785,13 +763,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(1);
   if(tid == 0)
   {
+    if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
     c_eng.carry_n[cur][z] = 0;
     c_eng.land_n[cur][z] = 0;
   }
   block_scan_zone_pair(s_cnt, s_ccnt, s_off, s_aux, s_tmp2);
-  // pending mail: the records counted (landing slots that hold a hole are not)
-  if(tid == 0 && s_tmp2[kZoneWaves - 1])
-    atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)s_tmp2[kZoneWaves - 1]);
   GPA_STAMP(2);
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
@@ -908,42 +884,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   int any_rem = 0;
 
-  // Planned sends: one chunk per local destination zone the last step sent
-  // at least kPlanMin records to (one atomic each, as the scatter's
-  // reservation would be). The bucket arrays after the histogram hold, until
-  // the behaviours are done, each chunk's record offset in land[nxt] (s_pb),
-  // the sends counted so far (s_cur) and the slots usable (s_lim); reserved
-  // slots past the destination's capacity go to the spill list as holes.
-  uint32_t* const s_pb = s_dyn + nb;
-  uint32_t* const s_cur = s_dyn + 2 * nb;
-  uint32_t* const s_lim = s_dyn + 3 * nb;
-  uint32_t n_res = 0, holes = 0;
-  {
-    const bool plan_in = GPA_PLAN && c_eng.plan_on[z] != 0u;
-    const uint16_t* prow = c_eng.plan + (size_t)z * nz;
-    for(uint32_t b = tid; b < nz; b += kZoneThreads)
-    {
-      uint32_t lim = 0, pb = 0;
-      const uint32_t h = plan_in ? prow[b] : 0u;
-      if(h >= kPlanMin && (int)h + kPlanSlack > 0)
-      {
-        const uint32_t r = (uint32_t)((int)h + kPlanSlack);
-        const uint32_t base = atomicAdd(&c_eng.land_n[nxt][b], r);
-        const uint32_t capb = zone_capacity(b);
-        ++n_res;
-        lim = base < capb ? min(r, capb - base) : 0u;
-        pb = (uint32_t)c_eng.zoff[b] + base;
-        for(uint32_t k = lim; k < r; ++k)
-          spill_rec(nxt, 0u, b, base + k, make_uint4(kHole, 0u, 0u, 0u));
-        holes += r - lim;
-      }
-      s_cur[b] = 0;
-      s_lim[b] = lim;
-      s_pb[b] = pb;
-    }
-  }
-  __syncthreads();
-
   // ---- 3. run handlers -------------------------------------------------------------
   ZoneCtx a;
   a.reset_common();
@@ -952,11 +892,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   a.ocap = cap;
   a.nxt = nxt;
   a.s_hist = s_hist;
-  a.s_cur = s_cur;
-  a.s_lim = s_lim;
-  a.s_pb = s_pb;
-  a.land_nxt = c_eng.land[nxt];
-  a.n_zones = GPA_PLAN ? nz : 0u;
   a.agg = &s_agg[wv];
   // fan-in senders fold their analyzer applies per zone in LDS
   if constexpr(kFan)
@@ -1059,36 +994,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     atomicAdd(&s_bytype[a.applied_type], (unsigned long long)applied);
   // ---- 3b. carry-out: every actor's unhandled remainder, canonical, to the
   //      next step's carry buffer (none in the usual step) -----------------------------
-  const bool any_rem_z = __syncthreads_or(any_rem);
-  // ---- 3a. planned chunks: unfilled slots become holes; the plan for the
-  //      next step is this step's sends per local destination zone ---------------------
-  if(GPA_PLAN)
-  {
-    int on = 0;
-    for(uint32_t b = tid; b < nz; b += kZoneThreads)
-    {
-      const uint32_t c = s_cur[b], lim = s_lim[b];
-      if(c < lim)
-      {
-        ZRec* d = c_eng.land[nxt] + s_pb[b];
-        for(uint32_t k = c; k < lim; ++k) d[k].w0 = kHole;
-        holes += lim - c;
-      }
-      on |= c >= kPlanMin;
-    }
-    if(holes) atomicAdd(&s_holes, holes);
-    if(__syncthreads_or(on))
-    {
-      uint16_t* prow = c_eng.plan + (size_t)z * nz;
-      for(uint32_t b = tid; b < nz; b += kZoneThreads) prow[b] = (uint16_t)min(s_cur[b], 0xFFFFu);
-      if(tid == 0) c_eng.plan_on[z] = 1u;
-    }
-    else if(tid == 0)
-      c_eng.plan_on[z] = 0u;
-    if(tid == 0 && s_holes) atomicAdd(&c_eng.hole_n[nxt], s_holes);
-  }
   uint32_t ncout = 0;
-  if(any_rem_z)
+  if(__syncthreads_or(any_rem))
   {
     ncout = block_scan_zone(s_aux, s_tmp);
     if(tid == 0) s_nbig = 0;
@@ -1172,7 +1079,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // ---- 4. one chunk per destination bucket ----------------------------------------
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
-  uint32_t n_atom = n_res;
+  uint32_t n_atom = 0;
   for(uint32_t b = tid; b < nb; b += kZoneThreads)
   {
     const uint32_t h = s_hist[b];
@@ -1314,8 +1221,6 @@ __global__ void __launch_bounds__(kBlock) k_pending(uint32_t cur, uint32_t slot)
   {
     unsigned long long tot = 0;
     for(int w = 0; w < kWaves; ++w) tot += s_red[w];
-    // landing slots that hold a hole (planned sends) are not mail
-    if(blockIdx.x == 0) tot -= c_eng.hole_n[cur];
     if(tot) atomicAdd(&c_eng.pend[slot], tot);
   }
 }

@@ -14,14 +14,7 @@ for v in "$@"; do
     base) b base ;;
     # single-table (pinger) experiment builds: ~30 s instead of ~3 min
     p512) b p512 -DGPA_STEP_ONLY=2 ;;
-    # the same without planned sends (every send through the outbox)
-    p512np) b p512np -DGPA_STEP_ONLY=2 -DGPA_PLAN=0 ;;
-    # reservation slack sweep (records per chunk beyond the last step's count)
-    ps0) b ps0 -DGPA_STEP_ONLY=2 -DGPA_PLAN_SLACK=0 ;;
-    psm3) b psm3 -DGPA_STEP_ONLY=2 -DGPA_PLAN_SLACK=-3 ;;
-    psm6) b psm6 -DGPA_STEP_ONLY=2 -DGPA_PLAN_SLACK=-6 ;;
     p1024) b p1024 -DGPA_STEP_ONLY=2 -DGPA_ZONE_THREADS=1024 ;;
-    p1024np) b p1024np -DGPA_STEP_ONLY=2 -DGPA_ZONE_THREADS=1024 -DGPA_PLAN=0 ;;
     z12a) b z12a -DGPA_ZONE_BITS=12 -DGPA_ZONE_THREADS=1024 -DGPA_IDX_CAP=24576 -DGPA_TILE=7168 ;;
     z12b) b z12b -DGPA_ZONE_BITS=12 -DGPA_ZONE_THREADS=1024 -DGPA_IDX_CAP=32768 -DGPA_TILE=8192 ;;
     *) echo "unknown variant $v"; exit 1 ;;
