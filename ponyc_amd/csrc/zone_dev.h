@@ -59,6 +59,18 @@ template <int HT> __host__ __device__ constexpr uint32_t small_regs()
           HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM) ? 16u : 8u;
 }
 
+// A workgroup barrier that orders LDS only. __syncthreads() also waits for
+// every global store the wave has in flight (vmcnt counts stores on CDNA);
+// inside a loop that scatters records to HBM between LDS phases, that wait
+// costs a full store latency per iteration. Use this one where the threads
+// share nothing through global memory across the barrier.
+__device__ __forceinline__ void lds_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
 #pragma unroll
@@ -152,7 +164,7 @@ __device__ void block_scan_zone_pair(const uint32_t* cnt, const uint32_t* ccnt, 
 
 // Exclusive scan of in[0, n) into out[0, n) (LDS) by a kZoneThreads workgroup,
 // each thread taking a contiguous run; returns the total. All threads call it;
-// it ends behind a barrier.
+// it ends behind a barrier (an LDS-only one: lds_sync).
 __device__ uint32_t block_scan_n(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* s_tmp)
 {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -162,18 +174,18 @@ __device__ uint32_t block_scan_n(const uint32_t* in, uint32_t* out, uint32_t n, 
   for(uint32_t i = lo; i < hi; ++i) sum += in[i];
   const uint32_t incl = wave_incl_scan(sum, lane);
   if(lane == 63) s_tmp[wv] = incl;
-  __syncthreads();
+  lds_sync();
   if(wv == 0)
   {
     uint32_t x = lane < (uint32_t)kZoneWaves ? s_tmp[lane] : 0u;
     x = wave_incl_scan(x, lane);
     if(lane < (uint32_t)kZoneWaves) s_tmp[lane] = x;
   }
-  __syncthreads();
+  lds_sync();
   uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
   for(uint32_t i = lo; i < hi; ++i) { const uint32_t v = in[i]; out[i] = run; run += v; }
   const uint32_t total = s_tmp[kZoneWaves - 1];
-  __syncthreads();
+  lds_sync();
   return total;
 }
 
@@ -284,6 +296,14 @@ struct AccS {
 // Groups handled whole up to this size keep their keys in registers.
 constexpr uint32_t kMedReg = 16;
 
+// A table whose behaviours ignore the message (the message-ubench pinger:
+// every ping has the same effect) needs no delivery order; the compiler then
+// drops the key selection of its drain entirely.
+template <int HT> __host__ __device__ constexpr bool order_free()
+{
+  return HT == GPU_ACTOR_HT_PINGER;
+}
+
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
   return HT == GPU_ACTOR_HT_FIFO_SINK;
@@ -294,6 +314,20 @@ template <int HT> __host__ __device__ constexpr bool may_yield()
 // behaviour whose sends muted the actor or that yielded. Returns how many ran;
 // the rest, [done, n) of acc, is left in canonical order for the carry-out
 // pass (the group is sorted in place when it was not handled whole).
+// The arrival group is handled, by its size:
+//   small  (<= SM, handled whole): all records loaded with the state, in
+//          registers; each message is the smallest key left (selection);
+//   medium (<= kMedReg, tables with SM < kMedReg): keys in registers, each
+//          record loaded again at its turn;
+//   window (handled whole, larger): a sorted register window of the SM
+//          smallest keys not yet handled (key << 16 | position), refilled by a
+//          pass over the group when it runs dry — g * ceil(g / SM) key loads instead of a g^2 selection
+//          from memory (C2-det: the ~15 actors per step with more than 16
+//          arrivals held their zones ~75 us, profiles/r03_general.txt);
+//   sorted (part of it carries over, or sorted by the workgroup): canonical
+//          order first, then in position order.
+// An order-free table (its behaviours ignore the message) handles a whole
+// group in position order: nothing is loaded for it.
 template <int HT, class Acc>
 __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, Acc acc,
   uint32_t n, uint32_t nc, bool presorted)
@@ -387,22 +421,58 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
         stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
     }
-    else if(q >= g && !presorted)
+    else if(!order_free<HT>() && q >= g && g <= 0xFFFFu && !presorted)
     {
-      // large group handled whole: select in key order
-      uint64_t last = 0;
+      // large group handled whole: key order through the window
+      uint64_t km[SM];
+#pragma unroll
+      for(int t = 0; t < (int)SM; ++t) km[t] = ~0ull;
+      uint64_t lo = 0;
       for(uint32_t r = 0; r < g && !stop; ++r)
       {
-        uint64_t best = ~0ull;
-        uint32_t bi = 0;
-        for(uint32_t j = 0; j < g; ++j)
+        if(km[0] == ~0ull)
         {
-          const uint64_t kk = zkey(acc.rec(nc + j));
-          if((r == 0 || kk > last) && kk < best) { best = kk; bi = j; }
+          // refill: the SM smallest keys >= lo, insertion-sorted
+          for(uint32_t j = 0; j < g; j += 4)
+          {
+            uint64_t kk[4];
+#pragma unroll
+            for(int u = 0; u < 4; ++u)
+              kk[u] = j + u < g ? zkey(acc.rec(nc + j + u)) : ~0ull;
+#pragma unroll
+            for(int u = 0; u < 4; ++u)
+            {
+              uint64_t x = (kk[u] << 16) | (j + u);
+              if(j + u >= g || kk[u] < lo || x >= km[SM - 1]) continue;
+#pragma unroll
+              for(int t = 0; t < (int)SM; ++t)
+              {
+                const uint64_t m = km[t];
+                const bool lt = x < m;
+                km[t] = lt ? x : m;
+                x = lt ? m : x;
+              }
+            }
+          }
         }
-        const ZRec rr = acc.rec(nc + bi);
+        const uint32_t pos = (uint32_t)km[0] & 0xFFFFu;
+        lo = (km[0] >> 16) + 1;
+#pragma unroll
+        for(int t = 0; t + 1 < (int)SM; ++t) km[t] = km[t + 1];
+        km[SM - 1] = ~0ull;
+        const ZRec rr = acc.rec(nc + pos);
         handle(HtTag<HT>{}, T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg);
-        last = best;
+        ++done;
+        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
+      }
+    }
+    else if(order_free<HT>() && q >= g && !presorted)
+    {
+      // order-free table, group handled whole: position order
+      for(uint32_t r = 0; r < g && !stop; ++r)
+      {
+        const ZRec rr = acc.rec(nc + r);
+        handle(HtTag<HT>{}, T, a, s, (rr.w0 >> 12) & 0xFu, rr.arg);
         ++done;
         stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
       }
@@ -478,9 +548,21 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
   for(uint32_t sh = lo; sh < hi; sh += 8)
   {
     for(uint32_t d = tid; d < 256; d += kZoneThreads) s_bin[d] = 0;
-    __syncthreads();
-    for(uint32_t i = tid; i < n; i += kZoneThreads) atomicAdd(&s_bin[(src[i] >> sh) & 255u], 1u);
-    __syncthreads();
+    lds_sync();
+    for(uint32_t i0 = 0; i0 < n; i0 += kZoneThreads * kUnroll)
+    {
+      uint64_t x[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        x[u] = i < n ? src[i] : 0ull;
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+        if(i0 + u * kZoneThreads + tid < n) atomicAdd(&s_bin[(x[u] >> sh) & 255u], 1u);
+    }
+    lds_sync();
     if(wv == 0)
     {
       uint32_t v[4], sum = 0;
@@ -491,11 +573,25 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
       for(int k = 0; k < 4; ++k) { s_bin[lane * 4 + k] = run; run += v[k]; }
     }
     uint32_t cb = 0;                       // which half of s_bin holds this tile's bases
+    // the items of kUnroll tiles are loaded together, then ranked tile by tile
+    uint64_t xs[kUnroll];
     for(uint32_t t0 = 0; t0 < n; t0 += kZoneThreads)
     {
+      const uint32_t tu = (t0 / kZoneThreads) % kUnroll;
+      if(tu == 0)
+      {
+#pragma unroll
+        for(int u = 0; u < kUnroll; ++u)
+        {
+          const uint32_t i = t0 + u * kZoneThreads + tid;
+          xs[u] = i < n ? src[i] : 0ull;
+        }
+      }
       const uint32_t i = t0 + tid;
       const bool valid = i < n;
-      const uint64_t x = valid ? src[i] : 0ull;
+      uint64_t x = xs[0];
+#pragma unroll
+      for(int u = 1; u < kUnroll; ++u) x = tu == (uint32_t)u ? xs[u] : x;
       const uint32_t d = (uint32_t)(x >> sh) & 255u;
       // lanes of this wave holding the same digit: 8 ballots
       uint64_t same = __ballot(valid);
@@ -509,7 +605,7 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
       __builtin_amdgcn_wave_barrier();
       const uint32_t rank = __popcll(same & lt);
       if(valid && rank == 0) s_wc[wv * 256 + d] = __popcll(same);
-      __syncthreads();                     // counts (and, first time, the bases) visible
+      lds_sync();                          // counts (and, first time, the bases) visible
       if(valid)
       {
         uint32_t pre = s_bin[cb * 256 + d];
@@ -523,8 +619,10 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
         s_bin[(cb ^ 1u) * 256 + k] = c;
       }
       cb ^= 1u;
-      __syncthreads();                     // every read of s_wc and the old bases done
+      lds_sync();                          // every read of s_wc and the old bases done
     }
+    // the pass's scattered stores are the next pass's loads (other threads)
+    __syncthreads();
     uint64_t* t = src; src = dst; dst = t;
   }
   if(src != a)
@@ -550,10 +648,23 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
   const uint32_t tid = threadIdx.x;
   // key range: min/max sender, max sequence
   uint32_t fmin = 0xFFFFFFFFu, fmax = 0, smax = 0;
-  for(uint32_t j = tid; j < g; j += kZoneThreads)
+  // kUnroll records in flight per thread (a group is tens of thousands of
+  // records: one load per iteration would wait out a memory latency each time)
+  for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
   {
-    const ZRec r = acc.rec(nc + j);
-    fmin = min(fmin, r.from); fmax = max(fmax, r.from); smax = max(smax, r.w0 >> 16);
+    ZRec r[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t j = j0 + u * kZoneThreads + tid;
+      if(j < g) r[u] = acc.rec(nc + j);
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      if(j0 + u * kZoneThreads + tid < g)
+      {
+        fmin = min(fmin, r[u].from); fmax = max(fmax, r[u].from); smax = max(smax, r[u].w0 >> 16);
+      }
   }
   if(tid < 3) s_red3[tid] = tid == 0 ? 0xFFFFFFFFu : 0u;
   __syncthreads();
@@ -564,18 +675,45 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
   const uint32_t sbits = bits_for(smax), kbits = bits_for(fmax - fmin) + sbits;
   const uint32_t pay = idx ? 16u : kPayBits;
   if(kbits + pay > 64u) return false;
-  for(uint32_t j = tid; j < g; j += kZoneThreads)
+  for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
   {
-    const ZRec r = acc.rec(nc + j);
-    const uint64_t key = ((uint64_t)(r.from - fmin) << sbits) | (r.w0 >> 16);
-    ia[j] = (key << pay) | (idx ? (uint64_t)idx[nc + j] : (uint64_t)j);
+    ZRec r[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t j = j0 + u * kZoneThreads + tid;
+      if(j < g) r[u] = acc.rec(nc + j);
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t j = j0 + u * kZoneThreads + tid;
+      if(j >= g) continue;
+      const uint64_t key = ((uint64_t)(r[u].from - fmin) << sbits) | (r[u].w0 >> 16);
+      ia[j] = (key << pay) | (idx ? (uint64_t)idx[nc + j] : (uint64_t)j);
+    }
   }
   __syncthreads();
   coop_radix_sort(ia, ib, g, pay, pay + ((kbits + 7u) & ~7u), s_work);
   const uint64_t pm = (1ull << pay) - 1;
   if(idx)
   {
-    for(uint32_t j = tid; j < g; j += kZoneThreads) idx[nc + j] = (uint16_t)(ia[j] & pm);
+    for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
+    {
+      uint64_t x[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        x[u] = j < g ? ia[j] : 0ull;
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j < g) idx[nc + j] = (uint16_t)(x[u] & pm);
+      }
+    }
   }
   else
   {
@@ -774,10 +912,23 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
   // (the two forms apart: a record held across the branch went to scratch)
   if(use_idx)
-    for(uint32_t i = tid; i < nc; i += kZoneThreads)
+    for(uint32_t i0 = 0; i0 < nc; i0 += kZoneThreads * kUnroll)
     {
-      const uint32_t a = C[i].w0 & kZoneMask;
-      s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
+      uint32_t w[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        w[u] = i < nc ? C[i].w0 : 0u;
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        if(i >= nc) continue;
+        const uint32_t a = w[u] & kZoneMask;
+        s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
+      }
     }
   else
     for(uint32_t i = tid; i < nc; i += kZoneThreads)
@@ -1026,17 +1177,31 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
       const uint32_t n = s_cnt[i];
       ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
-      for(uint32_t j = tid; j < rem; j += kZoneThreads)
+      // kUnroll records in flight per thread
+      for(uint32_t j0 = 0; j0 < rem; j0 += kZoneThreads * kUnroll)
       {
-        const ZRec r = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
-                               : AccS{Sz + s_off[i]}.rec(n - rem + j);
-        uint4 u;
-        u.x = r.w0; u.y = r.from; u.z = (uint32_t)r.arg; u.w = (uint32_t)(r.arg >> 32);
-        const uint32_t pos = co + j;
-        if(pos < cap)
-          *reinterpret_cast<uint4*>(cout + pos) = u;
-        else
-          spill_rec(nxt, kSpillCarry, z, pos, u);
+        ZRec r[kUnroll];
+#pragma unroll
+        for(int uu = 0; uu < kUnroll; ++uu)
+        {
+          const uint32_t j = j0 + uu * kZoneThreads + tid;
+          if(j < rem)
+            r[uu] = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
+                            : AccS{Sz + s_off[i]}.rec(n - rem + j);
+        }
+#pragma unroll
+        for(int uu = 0; uu < kUnroll; ++uu)
+        {
+          const uint32_t j = j0 + uu * kZoneThreads + tid;
+          if(j >= rem) continue;
+          uint4 u;
+          u.x = r[uu].w0; u.y = r[uu].from; u.z = (uint32_t)r[uu].arg; u.w = (uint32_t)(r[uu].arg >> 32);
+          const uint32_t pos = co + j;
+          if(pos < cap)
+            *reinterpret_cast<uint4*>(cout + pos) = u;
+          else
+            spill_rec(nxt, kSpillCarry, z, pos, u);
+        }
       }
     }
   }
@@ -1156,7 +1321,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         rk[u] = atomicAdd(&s_tcnt[bk[u]], 1u);
       }
     }
-    __syncthreads();
+    // the tile loop shares only LDS across its barriers: the previous tile's
+    // landing stores drain while this one is sorted
+    lds_sync();
     (void)block_scan_n(s_tcnt, s_tst, nb, s_tmp);
 #pragma unroll
     for(int u = 0; u < kTilePer; ++u)
@@ -1164,20 +1331,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t i = u * kZoneThreads + tid;
       if(i < m) s_pool[s_tst[bk[u]] + rk[u]] = ov[u];
     }
-    __syncthreads();
+    lds_sync();
     for(uint32_t p = tid; p < m; p += kZoneThreads)
     {
       const uint4 r = s_pool[p];
       const uint32_t b = bucket_of(r.x);
       emit(r, b, s_base[b] + (p - s_tst[b]));
     }
-    __syncthreads();
+    lds_sync();
     for(uint32_t b = tid; b < nb; b += kZoneThreads)
     {
       s_base[b] += s_tcnt[b];
       s_tcnt[b] = 0;
     }
-    __syncthreads();
+    lds_sync();
   }
 
   // ---- counters: block reduction, one atomic per workgroup per counter ---------------
