@@ -83,7 +83,15 @@ def test_storm(engine_factory, oracle):
 @pytest.mark.parametrize("sources,sinks,bursts,m,batch,cap", [(64, 8, 10, 4, 0, 1024),
                                                               (40, 5, 6, 3, 7, 1024),
                                                               (16, 2, 5, 9, 4, 1024),
-                                                              (4, 2, 1, 600, 0, 2048)])
+                                                              (4, 2, 1, 600, 0, 2048),
+                                                              # arrival groups handled whole
+                                                              # through the key window: 50 one-
+                                                              # push senders; 56 and 96 from 8
+                                                              (200, 4, 3, 1, 0, 1024),
+                                                              (8, 1, 3, 7, 0, 1024),
+                                                              (16, 2, 3, 12, 0, 1024),
+                                                              # 128 > batch: sorted, part carried
+                                                              (16, 2, 3, 16, 0, 1024)])
 def test_fifo_order_exact(engine_factory, oracle, sources, sinks, bursts, m, batch, cap):
     """Order-sensitive fold: equal only if delivery order is exactly the
     canonical (sender, seq) order, including carry-over under a batch limit."""
@@ -92,7 +100,21 @@ def test_fifo_order_exact(engine_factory, oracle, sources, sinks, bursts, m, bat
                  lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=cap),
                  W.fifo_result)
     _assert_same(g, o)
-    assert g[2][2].sum() == 0          # no per-pair FIFO violations
+    # no per-pair FIFO violations (the sink tracks 8 senders: the count is
+    # meaningful up to 8 per sink; the fold above checks the order regardless)
+    if sources // sinks <= 8:
+        assert g[2][2].sum() == 0
+
+
+def test_det_large_groups(engine_factory, oracle):
+    """40 pings per pinger: most arrival groups exceed the 16 a lane holds in
+    registers and go through the sorted key window (zone_dev.h drain_zone).
+    The det pinger's state does not depend on order (the FIFO cases above
+    check order); this checks that the window hands every record over
+    exactly once, with the zones grown past mailbox_cap on the way."""
+    g, o = _both(engine_factory, oracle, lambda e: W.ubench(e, 256, 40, det=True, hops=12),
+                 W.ubench_result)
+    _assert_same(g, o)
 
 
 def test_run_max_steps_resume(engine_factory, oracle):
