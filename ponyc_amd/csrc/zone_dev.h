@@ -905,11 +905,46 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.carry_n[cur][z] = 0;
     c_eng.land_n[cur][z] = 0;
   }
+
+  // The zone's type when one type covers all of its slots, else -1. It is
+  // wave-uniform, so that type's fields (batch, state, params) come through
+  // scalar loads instead of a per-lane lookup chain.
+  int tz = -1;
+  for(uint32_t t = 0; t < c_eng.n_types; ++t)
+    if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
+      tz = (int)t;
+  tz = __builtin_amdgcn_readfirstlane(tz);
+
+  // An order-free table (its behaviours ignore the message: the message-ubench
+  // pinger) needs only each actor's message count when nothing can be left
+  // over this step: no actor anywhere triggers muting (so none is muted or
+  // mutes itself; none of this zone's carries a trigger byte either), and
+  // every actor's mail fits its batch. Its records are
+  // then never read — no segment scan, no index, no group sort. Otherwise
+  // the zone takes the general path below.
+  bool fast = false;
+  if constexpr(HTS >= 0 && order_free<HTS>())
+    if(!gate && ztc == 0 && tz >= 0)
+    {
+      const uint32_t bt = c_types[tz].prio ? 0xFFFFFFFFu : c_types[tz].batch;
+      int over = 0;
+      for(uint32_t i = tid; i < kZone; i += kZoneThreads) over |= s_cnt[i] + s_ccnt[i] > bt;
+      fast = !__syncthreads_or(over);
+    }
+  ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
+  if(fast)
+  {
+    // the actor's total (carried + landed); no group was sorted
+    for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_cnt[i] += s_ccnt[i];
+    for(uint32_t k = tid; k < kZone / 32; k += kZoneThreads) s_bigbits[k] = 0;
+    __syncthreads();
+  }
+  else
+  {
   block_scan_zone_pair(s_cnt, s_ccnt, s_off, s_aux, s_tmp2);
   GPA_STAMP(2);
 
   // ---- 2. place into the sorted inbox ---------------------------------------------
-  ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
   // (the two forms apart: a record held across the branch went to scratch)
   if(use_idx)
     for(uint32_t i0 = 0; i0 < nc; i0 += kZoneThreads * kUnroll)
@@ -1017,19 +1052,12 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       __syncthreads();
     }
   }
+  }   // general path
   GPA_STAMP(7);                          // diagnostic build: the hot-group sort ends
   auto big_sorted = [&](uint32_t i) __attribute__((always_inline)) {
     return ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
   };
 
-  // The zone's type when one type covers all of its slots, else -1. It is
-  // wave-uniform, so that type's fields (batch, state, params) come through
-  // scalar loads instead of a per-lane lookup chain.
-  int tz = -1;
-  for(uint32_t t = 0; t < c_eng.n_types; ++t)
-    if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
-      tz = (int)t;
-  tz = __builtin_amdgcn_readfirstlane(tz);
 
   // s_aux will hold each actor's unhandled remainder (known after it ran)
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
