@@ -106,6 +106,18 @@ def test_fifo_order_exact(engine_factory, oracle, sources, sinks, bursts, m, bat
         assert g[2][2].sum() == 0
 
 
+@pytest.mark.parametrize("n,initial,budget,batch", [(512, 40, 60, 3), (3000, 12, 30, 5),
+                                                      (64, 300, 400, 100)])
+def test_ubench_faithful_batch_limit(engine_factory, oracle, n, initial, budget, batch):
+    """The pinger (an order-free table) past its batch: mail is carried, actors
+    overload and their senders are muted, so zones leave the count-only fast
+    path (zone_dev.h k_step) and come back to it as the backlogs drain; with
+    300 pings per pinger the groups are also past the batch and big."""
+    g, o = _both(engine_factory, oracle,
+                 lambda e: W.ubench(e, n, initial, budget, batch=batch), W.ubench_result)
+    _assert_same(g, o)
+
+
 def test_det_large_groups(engine_factory, oracle):
     """40 pings per pinger: most arrival groups exceed the 16 a lane holds in
     registers and go through the sorted key window (zone_dev.h drain_zone).
