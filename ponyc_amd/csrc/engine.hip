@@ -27,6 +27,18 @@
 #include "sparse_dev.h"
 #include "step_entry.h"
 
+// the 4096-actor-zone instantiations (step_*_z12.hip)
+namespace gpa_z12 {
+StepEntry step_entry_any();
+StepEntry step_entry_ring();
+StepEntry step_entry_pinger();
+StepEntry step_entry_pinger_det();
+StepEntry step_entry_fanin_sender();
+StepEntry step_entry_gups_streamer();
+StepEntry step_entry_storm();
+StepEntry step_entry_spreader();
+} // namespace gpa_z12
+
 using namespace gpa;
 
 // gups Updater tables (gups_basic/main.pony:145-155: table[k] = k + index*size),
@@ -316,6 +328,9 @@ struct Engine {
   SparseCtl* d_ctl = nullptr;
   SparseCtl* h_ctl = nullptr;             // pinned
   uint64_t sparse_launches = 0, sparse_steps = 0;
+  // zone geometry: actors per zone = 1 << zbits (step_entry.h; chosen by
+  // relayout_zones)
+  uint32_t zbits = kZoneBits;
 };
 
 Engine g;
@@ -352,6 +367,9 @@ inline uint64_t owned_below(uint64_t x)
 
 inline uint32_t blocks_for(uint64_t n, uint32_t bs = kBlock) { return (uint32_t)((n + bs - 1) / bs); }
 
+// actors per zone in this engine's geometry
+inline uint32_t zone_actors() { return 1u << g.zbits; }
+
 inline bool reducible_ht(uint32_t ht)
 {
   return ht == GPU_ACTOR_HT_FANIN_ANALYZER || ht == GPU_ACTOR_HT_GUPS_UPDATER;
@@ -360,9 +378,13 @@ inline bool reducible_ht(uint32_t ht)
 const std::vector<StepEntry>& step_entries()
 {
   static const std::vector<StepEntry> v = {
-    step_entry_any(), step_entry_ring(), step_entry_pinger(), step_entry_pinger_det(),
-    step_entry_fanin_sender(), step_entry_gups_streamer(), step_entry_storm(),
-    step_entry_spreader()};
+    gpa::step_entry_any(), gpa::step_entry_ring(), gpa::step_entry_pinger(),
+    gpa::step_entry_pinger_det(), gpa::step_entry_fanin_sender(),
+    gpa::step_entry_gups_streamer(), gpa::step_entry_storm(), gpa::step_entry_spreader(),
+    gpa_z12::step_entry_any(), gpa_z12::step_entry_ring(), gpa_z12::step_entry_pinger(),
+    gpa_z12::step_entry_pinger_det(), gpa_z12::step_entry_fanin_sender(),
+    gpa_z12::step_entry_gups_streamer(), gpa_z12::step_entry_storm(),
+    gpa_z12::step_entry_spreader()};
   return v;
 }
 
@@ -417,6 +439,7 @@ int upload_types()
   e.skipped = g.d_sstat ? &g.d_sstat->skipped : nullptr;
   e.spill_cap = g.spill_cap;
   e.xspill = g.d_xspill; e.xspill_n = g.d_xspill_n; e.xspill_cap = g.xspill_cap;
+  e.zbits = g.zbits;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -527,9 +550,59 @@ int fixup_spill()
 // Re-lay the zone buffers after actors were created: zone z holds
 // Σ_{serial actors in z} cap(type) records. Capacities only grow, so mail
 // already landed or carried is copied zone by zone into the new layout.
+// The zone geometry for n local actors (step_entry.h): 2048-actor zones with
+// two 512-thread workgroups per CU while the buckets are few; past ~640
+// buckets their four LDS bucket arrays no longer leave room for two
+// workgroups per CU, and 4096-actor zones (half the buckets, twice the run
+// length per bucket, one 1024-thread workgroup per CU) are faster — C5's 8M
+// actors: 2.20 -> 1.58 ms per step (profiles/r03_general.txt). Their LDS
+// holds up to ~2300 buckets.
+uint32_t pick_zone_bits(uint64_t n)
+{
+  const uint64_t rb = R() > 1 ? R() : 0;
+  const uint64_t nz11 = (n + 2047) / 2048, nz12 = (n + 4095) / 4096;
+  if(const char* f = getenv("PONYC_AMD_ZONE_BITS"))      // test hook: force a geometry
+    return atoi(f) == 12 ? 12u : 11u;
+  return (nz11 + rb > 640 && nz12 + rb <= 2300) ? 12u : 11u;
+}
+
+// No mail anywhere (landing or carried, either parity): a geometry change
+// then moves nothing.
+bool zones_empty()
+{
+  if(g.n_zones == 0) return true;
+  std::vector<uint32_t> v(g.n_zones);
+  for(int p = 0; p < 2; ++p)
+    for(uint32_t* src : {g.d_land_n[p], g.d_carry_n[p]})
+    {
+      if(hipMemcpy(v.data(), src, g.n_zones * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+      for(uint32_t x : v)
+        if(x) return false;
+    }
+  return true;
+}
+
 int relayout_zones()
 {
-  const uint32_t nz = (uint32_t)((g.n_local + kZone - 1) / kZone);
+  // the geometry may change only before any step ran, with no mail landed
+  // (zone buffers are copied zone by zone below)
+  bool fresh = false;
+  {
+    const uint32_t want = pick_zone_bits(g.n_local);
+    if(want != g.zbits && g.steps_total == 0 && g.sparse_launches == 0)
+    {
+      HIPCK(hipStreamSynchronize(g.stream));
+      if(zones_empty())
+      {
+        g.zbits = want;
+        g.zcap_min.clear();
+        fresh = true;
+      }
+    }
+  }
+  const uint32_t za = zone_actors();
+  const uint32_t nz = (uint32_t)((g.n_local + za - 1) / za);
   if(nz > kMaxZones) return GPU_ACTOR_ERANGE;
   std::vector<uint64_t> cap64(nz, 0);
   for(const HostType& t : g.types)
@@ -537,8 +610,8 @@ int relayout_zones()
     if(!t.created || reducible_ht(t.ht)) continue;
     for(uint64_t L = t.lfirst; L < (uint64_t)t.lfirst + t.lcount; )
     {
-      const uint64_t z = L / kZone;
-      const uint64_t hi = std::min<uint64_t>((z + 1) * kZone, (uint64_t)t.lfirst + t.lcount);
+      const uint64_t z = L / za;
+      const uint64_t hi = std::min<uint64_t>((z + 1) * za, (uint64_t)t.lfirst + t.lcount);
       cap64[z] += (hi - L) * t.cap;
       L = hi;
     }
@@ -572,7 +645,7 @@ int relayout_zones()
     HIPCK(hipMalloc(&cn, std::max<size_t>(nz, 1) * sizeof(uint32_t)));
     HIPCK(hipMemsetAsync(ln, 0, std::max<size_t>(nz, 1) * sizeof(uint32_t), g.stream));
     HIPCK(hipMemsetAsync(cn, 0, std::max<size_t>(nz, 1) * sizeof(uint32_t), g.stream));
-    if(g.n_zones)
+    if(g.n_zones && !fresh)
     {
       hipLaunchKernelGGL(k_zone_copy, dim3(g.n_zones), dim3(kBlock), 0, g.stream,
         (const ZRec*)g.d_land[p], g.d_zoff, g.d_zcap, land, (const uint64_t*)d_off);
@@ -603,7 +676,7 @@ int relayout_zones()
   g.n_zones = nz;
   g.zcap_host = cap;
   // the receiver each muted actor waits on, one word per local slot
-  const uint64_t slots = (uint64_t)nz * kZone;
+  const uint64_t slots = (uint64_t)nz * za;
   if(slots > g.muted_on_cap)
   {
     uint32_t* mo = nullptr;
@@ -779,8 +852,8 @@ int exchange_room(uint64_t max_send, uint64_t total_recv, uint64_t xs)
 uint64_t trig_live_bytes()
 {
   const uint64_t per_rank = (g.n_actors + R() - 1) / R();
-  const uint64_t zones = (per_rank + kZone - 1) / kZone;
-  return std::min<uint64_t>(g.trig_bytes, (zones * kZone * R() + 7) & ~7ull);
+  const uint64_t zones = (per_rank + zone_actors() - 1) / zone_actors();
+  return std::min<uint64_t>(g.trig_bytes, (zones * zone_actors() * R() + 7) & ~7ull);
 }
 
 int exchange_step(uint32_t step_sidx)
@@ -931,22 +1004,28 @@ int exchange_step(uint32_t step_sidx)
 StepEntry pick_step_entry()
 {
   int only = -1;
+  bool mixed = false;
   for(const HostType& t : g.types)
   {
     if(!t.created || reducible_ht(t.ht)) continue;
-    if(only >= 0 && (uint32_t)only != t.ht) return step_entry_any();
+    if(only >= 0 && (uint32_t)only != t.ht) mixed = true;
     only = (int)t.ht;
   }
+  if(mixed) only = -1;
+  const bool z12 = g.zbits == 12;
   switch(only)
   {
-    case GPU_ACTOR_HT_RING: return step_entry_ring();
-    case GPU_ACTOR_HT_PINGER: return step_entry_pinger();
-    case GPU_ACTOR_HT_PINGER_DET: return step_entry_pinger_det();
-    case GPU_ACTOR_HT_FANIN_SENDER: return step_entry_fanin_sender();
-    case GPU_ACTOR_HT_GUPS_STREAMER: return step_entry_gups_streamer();
-    case GPU_ACTOR_HT_STORM: return step_entry_storm();
-    case GPU_ACTOR_HT_SPREADER: return step_entry_spreader();
-    default: return step_entry_any();
+    case GPU_ACTOR_HT_RING: return z12 ? gpa_z12::step_entry_ring() : gpa::step_entry_ring();
+    case GPU_ACTOR_HT_PINGER: return z12 ? gpa_z12::step_entry_pinger() : gpa::step_entry_pinger();
+    case GPU_ACTOR_HT_PINGER_DET:
+      return z12 ? gpa_z12::step_entry_pinger_det() : gpa::step_entry_pinger_det();
+    case GPU_ACTOR_HT_FANIN_SENDER:
+      return z12 ? gpa_z12::step_entry_fanin_sender() : gpa::step_entry_fanin_sender();
+    case GPU_ACTOR_HT_GUPS_STREAMER:
+      return z12 ? gpa_z12::step_entry_gups_streamer() : gpa::step_entry_gups_streamer();
+    case GPU_ACTOR_HT_STORM: return z12 ? gpa_z12::step_entry_storm() : gpa::step_entry_storm();
+    case GPU_ACTOR_HT_SPREADER: return z12 ? gpa_z12::step_entry_spreader() : gpa::step_entry_spreader();
+    default: return z12 ? gpa_z12::step_entry_any() : gpa::step_entry_any();
   }
 }
 
@@ -1104,21 +1183,21 @@ int spawn_process(uint32_t cur)
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
-  // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
-  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
-                                                          kSortWork);
   const StepEntry se = pick_step_entry();
   if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
+  // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
+  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
+                                                          se.sort_work);
   step_kernel_t kern = se.kernel;
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
-    hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), (uint32_t)dyn, g.stream,
+    hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
       e0, e1, 0u, g.par, slot, g.sidx);
   }
   else
-    hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(kZoneThreads), dyn, g.stream, g.par, slot, g.sidx);
+    hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
   HIPCK(hipGetLastError());
   const uint32_t step_sidx = g.sidx;
   g.par ^= 1u;
@@ -1365,7 +1444,7 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipHostMalloc(&g.h_sstat, sizeof(Engine::SpillStat), hipHostMallocDefault));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   HIPCK(hipMalloc(&g.d_need, kMaxZones * sizeof(uint32_t)));
-  g.trig_bytes = (g.cfg.max_actors + 2 * kZone + 7) & ~7ull;
+  g.trig_bytes = (g.cfg.max_actors + 2 * 4096 + 7) & ~7ull;   // room for either zone size
   for(int p = 0; p < 2; ++p)
   {
     HIPCK(hipMalloc(&g.d_trig[p], g.trig_bytes));
@@ -1478,6 +1557,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   for(auto& t : g.types) t = HostType();
   g.init = false; g.n_types = 0; g.n_actors = 0; g.n_local = 0;
   g.n_zones = 0; g.zone_records = 0; g.d_zoff = nullptr; g.d_zcap = nullptr; g.par = 0;
+  g.zbits = kZoneBits;
   for(int p = 0; p < 2; ++p)
   {
     g.d_land[p] = g.d_carry[p] = nullptr;

@@ -2,7 +2,8 @@
 // tables of the gpu_actor engine. See DESIGN.md for the rationale.
 //
 // HBM layout (per rank; actor id a lives on rank a % R at local slot L = a / R):
-//   Local slots are cut into zones of kZone (2048) actors. Zone z owns
+//   Local slots are cut into zones of kZone actors (2048, or 4096 for large
+//   engines: step_entry.h). Zone z owns
 //     land[p][z]   : landing buffer of step-p arrivals (unordered 16-B ZRecs),
 //                    filled by producers in chunks, one atomicAdd on
 //                    land_n[p][z] per (producer zone, destination zone);
@@ -30,13 +31,13 @@ constexpr int      kWaves = kBlock / 64;
 #ifndef GPA_ZONE_THREADS
 #define GPA_ZONE_THREADS 512
 #endif
-constexpr int      kZoneBits = GPA_ZONE_BITS;    // to_local field holds up to 12 bits
+constexpr int      kZoneBits = GPA_ZONE_BITS;    // this code object's k_step geometry; to_local holds up to 12 bits
 static_assert(kZoneBits <= 12, "to_local is 12 bits of a ZRec's w0");
 constexpr uint32_t kZone = 1u << kZoneBits;      // actors per zone
 constexpr uint32_t kZoneMask = kZone - 1;
 constexpr int      kZoneThreads = GPA_ZONE_THREADS;  // one workgroup per zone
 constexpr int      kZoneWaves = kZoneThreads / 64;
-constexpr uint32_t kMaxZones = 4096;             // histogram bound (8M actors/rank)
+constexpr uint32_t kMaxZones = 4096;             // histogram bound (zones per rank)
 constexpr uint32_t kMaxRanks = 64;
 constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above every actor
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
@@ -167,6 +168,10 @@ struct EngDev {
   XSpillRec* xspill;
   unsigned int* xspill_n;
   uint32_t xspill_cap, pad5;
+  // zone geometry of this engine (step_entry.h): actors per zone = 1 << zbits.
+  // k_step is compiled per geometry (kZoneBits below is its own); the helper
+  // kernels and the small-step path read it here.
+  uint32_t zbits, pad6;
 };
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -205,6 +210,10 @@ __device__ __forceinline__ uint32_t zone_capacity(uint32_t z)
   return c_eng.zcapz[z];
 }
 
+// zone of a local slot, and the slot within its zone (this engine's geometry)
+__device__ __forceinline__ uint32_t zone_of_local(uint32_t L) { return L >> c_eng.zbits; }
+__device__ __forceinline__ uint32_t slot_in_zone(uint32_t L) { return L & ((1u << c_eng.zbits) - 1u); }
+
 // outbox bucket of a destination: its zone, or n_zones + peer rank if remote
 __device__ __forceinline__ uint32_t bucket_of(uint32_t to)
 {
@@ -214,7 +223,7 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t to)
     const uint32_t owner = rmod(to);
     if(owner != c_eng.rank) return c_eng.n_zones + owner;
   }
-  return rdiv(to) >> kZoneBits;
+  return zone_of_local(rdiv(to));
 }
 
 // Cross-rank record from global ids and a (seq << 16 | beh << 12) word.
@@ -361,7 +370,7 @@ __device__ __forceinline__ void send_direct(uint32_t nxt, uint32_t self, uint32_
   {
     const uint32_t pos = atomicAdd(&c_eng.land_n[nxt][b], 1u);
     uint4 v;
-    v.x = w | (rdiv(to) & kZoneMask);
+    v.x = w | slot_in_zone(rdiv(to));
     v.y = self;
     v.z = (uint32_t)arg;
     v.w = (uint32_t)(arg >> 32);

@@ -99,10 +99,10 @@ __device__ void sp_land(const SpList& l, uint32_t n, uint32_t p)
   for(uint32_t i = threadIdx.x; i < n; i += kSpThreads)
   {
     const uint32_t L = (uint32_t)(l.K[i] >> 32);
-    const uint32_t z = L >> kZoneBits;
+    const uint32_t z = zone_of_local(L);
     const uint32_t pos = atomicAdd(&c_eng.land_n[p][z], 1u);
     uint4 v;
-    v.x = l.W[i] | (L & kZoneMask);
+    v.x = l.W[i] | slot_in_zone(L);
     v.y = (uint32_t)l.K[i];
     v.z = (uint32_t)l.A[i];
     v.w = (uint32_t)(l.A[i] >> 32);
@@ -240,8 +240,9 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     uint32_t lo = 0, hi = nz;          // zone z with s_zpre[z] <= i < s_zpre[z + 1]
     while(hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if(s_zpre[m] <= i) lo = m; else hi = m; }
     const uint4 v = *reinterpret_cast<const uint4*>(c_eng.land[cur] + c_eng.zoff[lo] + (i - s_zpre[lo]));
-    bK[0][i] = ((uint64_t)(lo * kZone + (v.x & kZoneMask)) << 32) | v.y;
-    bW[0][i] = v.x & ~kZoneMask;
+    const uint32_t zm = (1u << c_eng.zbits) - 1u;
+    bK[0][i] = ((uint64_t)((lo << c_eng.zbits) + (v.x & zm)) << 32) | v.y;
+    bW[0][i] = v.x & ~zm;
     bA[0][i] = ((uint64_t)v.w << 32) | v.z;
   }
   for(uint32_t z = z0; z < z1; ++z) c_eng.land_n[cur][z] = 0;
@@ -251,7 +252,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
   for(uint32_t z = z0; z < z1; ++z)
     if(c_eng.ztrig[cur ^ 1u][z])
     {
-      const uint32_t L0 = z * kZone, nact = min(kZone, c_eng.n_local - L0);
+      const uint32_t zs = 1u << c_eng.zbits;
+      const uint32_t L0 = z * zs, nact = min(zs, c_eng.n_local - L0);
       for(uint32_t i = 0; i < nact; ++i) c_eng.trig_own[cur ^ 1u][L0 + i] = 0;
       c_eng.ztrig[cur ^ 1u][z] = 0;
     }
@@ -398,7 +400,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       SparseCtx a;
       a.reset_common();
       a.self = L * c_eng.nranks + c_eng.rank;
-      a.src_local = L & kZoneMask;
+      a.src_local = slot_in_zone(L);
       a.type = t;
       a.agg = &s_agg[wv];
       a.nx = Bnxt;

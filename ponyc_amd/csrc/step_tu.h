@@ -1,6 +1,8 @@
 // step_tu.h — body of one k_step translation unit (step_*.hip): instantiates
 // k_step<GPA_STEP_HT> and exports it with the upload of this code object's
-// engine constants.
+// engine constants. A step_*_z12.hip unit first sets the 4096-actor zone
+// geometry and renames the namespace (gpa -> gpa_z12), so both geometries'
+// kernels link into one library.
 #define GPA_STEP_TU 1
 #include "zone_dev.h"
 #include "step_entry.h"
@@ -19,7 +21,7 @@ template __global__ void k_step<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
 #endif
 
 namespace {
-hipError_t step_upload(const TypeDev* types, const EngDev* eng, hipStream_t s)
+hipError_t step_upload(const void* types, const void* eng, hipStream_t s)
 {
   const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_types), types,
     sizeof(TypeDev) * GPU_ACTOR_MAX_TYPES, 0, hipMemcpyHostToDevice, s);
@@ -29,9 +31,11 @@ hipError_t step_upload(const TypeDev* types, const EngDev* eng, hipStream_t s)
 } // namespace
 
 #if GPA_STEP_STUB
-StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true }; }
+StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true, (uint32_t)kZoneBits,
+                                      (uint32_t)kZoneThreads, kSortWork }; }
 #else
-StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload, false }; }
+StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload, false, (uint32_t)kZoneBits,
+                                      (uint32_t)kZoneThreads, kSortWork }; }
 #endif
 
 } // namespace gpa

@@ -1448,7 +1448,7 @@ __device__ __forceinline__ void land_records(LandRec (&r)[kLandPer], uint32_t cu
   for(int u = 0; u < kLandPer; ++u)
     if(r[u].valid)
     {
-      zt[u] = rdiv(r[u].to) >> kZoneBits;
+      zt[u] = zone_of_local(rdiv(r[u].to));
       rk[u] = atomicAdd(&s_hist[zt[u]], 1u);
     }
   __syncthreads();
@@ -1461,7 +1461,7 @@ __device__ __forceinline__ void land_records(LandRec (&r)[kLandPer], uint32_t cu
     {
       const uint32_t pos = s_base[zt[u]] + rk[u];
       uint4 v;
-      v.x = r[u].w | (rdiv(r[u].to) & kZoneMask);
+      v.x = r[u].w | slot_in_zone(rdiv(r[u].to));
       v.y = r[u].from;
       v.z = (uint32_t)r[u].arg;
       v.w = (uint32_t)(r[u].arg >> 32);

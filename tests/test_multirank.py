@@ -55,3 +55,13 @@ def test_two_ranks_one_gpu(case):
     assert r["pending"][0] == r["pending"][1]
     assert r["by_type"]
     assert case == "ring1" or r["remote"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ubench_det", "storm", "spreader", "mute", "spill_one_rank",
+                                  "xspill"])
+def test_two_ranks_zones_4096(case, monkeypatch):
+    """The same two-rank parity cases with 4096-actor zones forced
+    (engine.hip: pick_zone_bits), as large engines run them."""
+    monkeypatch.setenv("PONYC_AMD_ZONE_BITS", "12")
+    test_two_ranks_one_gpu(case)
