@@ -271,24 +271,34 @@ struct AccIdx {
   }
 };
 
+// AccS: the actor's carried mail read in place from the carry buffer (it is
+// grouped by actor, in canonical order: no copy), its arrivals materialised
+// in the zone scratch S.
 struct AccS {
-  ZRec* p;
-  __device__ __forceinline__ ZRec rec(uint32_t j) const { return ld_rec(p + j); }
+  ZRec* p;            // arrivals: p[0, g)
+  const ZRec* c;      // carried mail: c[0, nc)
+  uint32_t nc;
+  __device__ __forceinline__ ZRec rec(uint32_t j) const
+  {
+    return j < nc ? ld_rec(c + j) : ld_rec(p + (j - nc));
+  }
+  // insertion sort of the arrival group [lo, lo + g), lo == nc
   __device__ void sort(uint32_t lo, uint32_t g)
   {
+    ZRec* q = p + (lo - nc);
     for(uint32_t i = 1; i < g; ++i)
     {
-      const ZRec x = p[lo + i];
+      const ZRec x = q[i];
       const uint64_t kx = zkey(x);
       uint32_t j = i;
       while(j > 0)
       {
-        const ZRec y = p[lo + j - 1];
+        const ZRec y = q[j - 1];
         if(zkey(y) <= kx) break;
-        p[lo + j] = y;
+        q[j] = y;
         --j;
       }
-      p[lo + j] = x;
+      q[j] = x;
     }
   }
 };
@@ -639,8 +649,9 @@ __device__ __forceinline__ uint32_t bits_for(uint32_t v)
 
 // Sort the arrival group [nc, nc + g) of one actor's segment, by the whole
 // workgroup. idx path: payload = the idx entry; S path: payload = position,
-// and the records are permuted through scratch `tmp` (g records). Returns
-// false (nothing changed) when the compressed key does not fit.
+// and the arrivals (seg[0, g)) are permuted through scratch `tmp` (g
+// records). Returns false (nothing changed) when the compressed key does not
+// fit.
 template <class Acc>
 __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, uint32_t g,
   uint64_t* ia, uint64_t* ib, ZRec* tmp, uint32_t* s_work, uint32_t* s_red3)
@@ -717,9 +728,9 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
   }
   else
   {
-    for(uint32_t j = tid; j < g; j += kZoneThreads) tmp[j] = seg[nc + (uint32_t)(ia[j] & pm)];
+    for(uint32_t j = tid; j < g; j += kZoneThreads) tmp[j] = seg[(uint32_t)(ia[j] & pm)];
     __syncthreads();
-    for(uint32_t j = tid; j < g; j += kZoneThreads) seg[nc + j] = tmp[j];
+    for(uint32_t j = tid; j < g; j += kZoneThreads) seg[j] = tmp[j];
   }
   __syncthreads();
   return true;
@@ -756,6 +767,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   uint32_t* const s_ccnt = s_off + kZone;   // carried records per actor
   uint32_t* const s_aux = s_ccnt + kZone;   // carry start -> landing cursor -> carry-out offset
   uint16_t* const s_idx = reinterpret_cast<uint16_t*>(s_aux + kZone);  // index into carry ++ landing
+  uint32_t* const s_cst = reinterpret_cast<uint32_t*>(s_idx);   // S path: carry start per actor
   extern __shared__ uint32_t s_dyn[];   // [nb] histogram, [nb] chunk bases, [nb] tile counts, [nb] tile starts
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
   __shared__ uint32_t s_tmp2[2 * kZoneWaves];
@@ -965,13 +977,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         s_idx[s_off[a] + (i - s_aux[a])] = (uint16_t)i;
       }
     }
-  else
-    for(uint32_t i = tid; i < nc; i += kZoneThreads)
-    {
-      const uint4 r = *reinterpret_cast<const uint4*>(C + i);
-      const uint32_t a = r.x & kZoneMask;
-      *reinterpret_cast<uint4*>(Sz + s_off[a] + (i - s_aux[a])) = r;
-    }
+  // (S path: carried mail stays where it is, read in place through AccS)
   if(use_idx)
   {
     // LDS index only: records stay in the landing buffer
@@ -985,8 +991,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
   else
   {
+    // each actor's carry start moves to s_cst (the index area, unused on this
+    // path) and its S segment holds only arrivals: scan(cnt + ccnt) - scan(ccnt)
     __syncthreads();
-    for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
+    for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+    {
+      s_cst[i] = s_aux[i];
+      s_off[i] -= s_aux[i];
+      s_aux[i] = 0;
+    }
     __syncthreads();
     for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
     {
@@ -1005,7 +1018,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       {
         if(r[u].x == 0xFFFFFFFFu) continue;
         const uint32_t a = r[u].x & kZoneMask;
-        pos[u] = s_off[a] + s_ccnt[a] + atomicAdd(&s_aux[a], 1u);
+        pos[u] = s_off[a] + atomicAdd(&s_aux[a], 1u);
       }
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
@@ -1044,7 +1057,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           ok = coop_sort_group(AccIdx{s_idx + s_off[i], C, Ld, nc}, s_idx + s_off[i], nullptr,
                                s_ccnt[i], g, ia, ia + g, nullptr, s_dyn, s_red3);
         else
-          ok = coop_sort_group(AccS{Sz + s_off[i]}, nullptr, Sz + s_off[i], s_ccnt[i], g, ia,
+          ok = coop_sort_group(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, nullptr, Sz + s_off[i],
+                               s_ccnt[i], g, ia,
                                ia + g, Sz + 2 * cap, s_dyn, s_red3);
         if(ok && tid == 0) s_bigbits[i >> 5] |= 1u << (i & 31);
       }
@@ -1107,7 +1121,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
     }                                                                                 \
     else                                                                              \
-      d = zone_actor<HT>(T, a, AccS{Sz + s_off[i]}, n, s_ccnt[i], stays, big_sorted(i));
+    {                                                                                 \
+      AccS acc{Sz + s_off[i], C + s_cst[i], s_ccnt[i]};                               \
+      d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
+    }
     if constexpr(HTS >= 0)
     {
       ZDRAIN(HTS)
@@ -1194,7 +1211,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       if(use_idx)
         carry_out(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
       else
-        carry_out(AccS{Sz + s_off[i]}, n - rem, n, z, co, nxt);
+        carry_out(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, n - rem, n, z, co, nxt);
     }
     __syncthreads();
     const uint32_t nbig = min(s_nbig, kMaxBig);
@@ -1215,7 +1232,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           const uint32_t j = j0 + uu * kZoneThreads + tid;
           if(j < rem)
             r[uu] = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
-                            : AccS{Sz + s_off[i]}.rec(n - rem + j);
+                            : AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}.rec(n - rem + j);
         }
 #pragma unroll
         for(int uu = 0; uu < kUnroll; ++uu)
