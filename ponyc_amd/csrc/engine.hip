@@ -198,6 +198,39 @@ __global__ void __launch_bounds__(kBlock) k_spill_place(const SpillRec* s, uint3
   base[c_eng.zoff[r.z] + (r.tag & kSpillPosMask)] = r.rec;
 }
 
+// Backlog copies listed by k_step (EngDev::bigc, defer_big): every workgroup
+// takes its stride of every listed copy, so one overloaded receiver's
+// remainder moves at the whole GPU's bandwidth instead of one CU's; the last
+// workgroup to finish clears the list for the next step.
+constexpr uint32_t kBigCopyCap = 4096;
+constexpr uint32_t kBigCopyBlocks = 512;
+__global__ void __launch_bounds__(kBlock) k_carry_big()
+{
+  const uint32_t n = min(c_eng.bigc_n[0], c_eng.bigc_cap);
+  const uint32_t stride = gridDim.x * kBlock;
+  for(uint32_t d = 0; d < n; ++d)
+  {
+    const BigCopy b = c_eng.bigc[d];
+    for(uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < b.rem; j += stride)
+    {
+      const uint32_t k = b.from + j;
+      const uint4 r = k < b.ncc ? *reinterpret_cast<const uint4*>(b.c + k)
+                                : *reinterpret_cast<const uint4*>(b.p + (k - b.ncc));
+      *reinterpret_cast<uint4*>(b.dst + j) = r;
+    }
+  }
+  __syncthreads();
+  if(threadIdx.x == 0)
+  {
+    __threadfence();
+    if(atomicAdd(&c_eng.bigc_n[1], 1u) == gridDim.x - 1)
+    {
+      atomicExch(&c_eng.bigc_n[0], 0u);
+      atomicExch(&c_eng.bigc_n[1], 0u);
+    }
+  }
+}
+
 // ===========================================================================
 // Host side
 // ===========================================================================
@@ -317,6 +350,10 @@ struct Engine {
   uint32_t* d_ztrig[2] = {nullptr, nullptr};
   unsigned int* d_trig_n = nullptr;
   uint32_t sidx = 0;
+  // backlog copies handed to k_carry_big (EngDev::bigc)
+  BigCopy* d_bigc = nullptr;
+  unsigned int* d_bigc_n = nullptr;
+  bool defer_big = false;
   SpillRec* d_spill[2] = {nullptr, nullptr};
   uint32_t spill_cap = 0;
   SpillStat* d_sstat = nullptr;
@@ -388,6 +425,19 @@ const std::vector<StepEntry>& step_entries()
   return v;
 }
 
+// Backlog copies go to k_carry_big when some serial type can leave mail over
+// in order (every table but the order-free pinger and the ring, whose token
+// never queues); elsewhere the extra launch per step would buy nothing.
+// PONYC_AMD_DEFER_BIG=0/1 forces it (tests, A/B).
+bool defer_big_wanted()
+{
+  if(const char* f = getenv("PONYC_AMD_DEFER_BIG")) return atoi(f) != 0;
+  for(const HostType& t : g.types)
+    if(t.created && !reducible_ht(t.ht) && t.ht != GPU_ACTOR_HT_PINGER && t.ht != GPU_ACTOR_HT_RING)
+      return true;
+  return false;
+}
+
 int upload_types()
 {
   TypeDev td[GPU_ACTOR_MAX_TYPES];
@@ -440,6 +490,9 @@ int upload_types()
   e.spill_cap = g.spill_cap;
   e.xspill = g.d_xspill; e.xspill_n = g.d_xspill_n; e.xspill_cap = g.xspill_cap;
   e.zbits = g.zbits;
+  g.defer_big = defer_big_wanted();
+  e.bigc = g.d_bigc; e.bigc_n = g.d_bigc_n; e.bigc_cap = kBigCopyCap;
+  e.defer_big = g.defer_big ? 1u : 0u;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -1194,10 +1247,17 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
     hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
-      e0, e1, 0u, g.par, slot, g.sidx);
+      e0, g.defer_big ? nullptr : e1, 0u, g.par, slot, g.sidx);
+    if(g.defer_big)
+      hipExtLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream,
+        nullptr, e1, 0u);
   }
   else
+  {
     hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
+    if(g.defer_big)
+      hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream);
+  }
   HIPCK(hipGetLastError());
   const uint32_t step_sidx = g.sidx;
   g.par ^= 1u;
@@ -1300,6 +1360,8 @@ void free_all()
   }
   if(g.d_muted_on) (void)hipFree(g.d_muted_on);
   if(g.d_trig_n) (void)hipFree(g.d_trig_n);
+  if(g.d_bigc) (void)hipFree(g.d_bigc);
+  if(g.d_bigc_n) (void)hipFree(g.d_bigc_n);
   if(g.h_ctl) (void)hipHostFree(g.h_ctl);
   if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
@@ -1461,6 +1523,9 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMemsetAsync(g.d_spill_flag, 0, sizeof(unsigned int), g.stream));
   HIPCK(hipMalloc(&g.d_trig_n, 4 * sizeof(unsigned int)));
   HIPCK(hipMemsetAsync(g.d_trig_n, 0, 4 * sizeof(unsigned int), g.stream));
+  HIPCK(hipMalloc(&g.d_bigc, kBigCopyCap * sizeof(BigCopy)));
+  HIPCK(hipMalloc(&g.d_bigc_n, 2 * sizeof(unsigned int)));
+  HIPCK(hipMemsetAsync(g.d_bigc_n, 0, 2 * sizeof(unsigned int), g.stream));
   HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
   HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
@@ -1576,6 +1641,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
     g.trig_stale[p] = false;
   }
   g.trig_bytes = 0; g.d_muted_on = nullptr; g.muted_on_cap = 0; g.d_trig_n = nullptr; g.sidx = 0;
+  g.d_bigc = nullptr; g.d_bigc_n = nullptr; g.defer_big = false;
   g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;
   for(int p = 0; p < 2; ++p) g.d_skey[p] = g.d_sarg[p] = nullptr;
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;

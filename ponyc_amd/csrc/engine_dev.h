@@ -118,6 +118,17 @@ struct TypeDev {
   uint64_t  params[GPU_ACTOR_MAX_PARAMS];
 };
 
+// One deferred carry copy: records rec(from + j), j < rem, of an actor's
+// canonical mail (rec(k) = k < ncc ? c[k] : p[k - ncc]: its carried mail,
+// then its sorted arrivals) to dst[j].
+struct BigCopy {
+  const ZRec* c;
+  const ZRec* p;
+  ZRec* dst;
+  uint32_t ncc, from, rem, pad;
+};
+static_assert(sizeof(BigCopy) == 40, "BigCopy is 40 B");
+
 struct EngDev {
   uint32_t n_types, rank, nranks, n_local;
   uint32_t n_zones, pad0;
@@ -172,7 +183,16 @@ struct EngDev {
   // k_step is compiled per geometry (kZoneBits below is its own); the helper
   // kernels and the small-step path read it here.
   uint32_t zbits, pad6;
+  // backlogs handed to the whole GPU: with defer_big set, a
+  // zone whose actor leaves more than kBigGroup records over (an overloaded
+  // receiver) lists the copy here instead of making it with its own
+  // workgroup; k_carry_big, launched right behind k_step, copies every listed
+  // remainder across all CUs and clears the list.
+  BigCopy* bigc;
+  unsigned int* bigc_n;           // [2]: listed copies, finished k_carry_big workgroups
+  uint32_t bigc_cap, defer_big;
 };
+
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
 __constant__ EngDev  c_eng;

@@ -38,6 +38,7 @@ namespace gpa {
 #endif
 
 constexpr int kUnroll = 8;   // independent records in flight per thread in streaming loops
+constexpr uint32_t kCarryRun = 256;   // carry records per sample when a backlog is counted
 #ifndef GPA_IDX_CAP
 #define GPA_IDX_CAP 16384
 #endif
@@ -193,6 +194,10 @@ __device__ uint32_t block_scan_n(const uint32_t* in, uint32_t* out, uint32_t n, 
 // the lanes that added to the same counter (atomicAdd's return, in lane
 // order). The lanes of up to 4 distinct keys per wave are folded into one LDS
 // atomic each (carried backlogs, grouped by actor); the rest add one by one.
+// kMinRun > 0 (landed records, usually spread over the zone): folding stops
+// at the first key held by fewer lanes than that — only a hot receiver's
+// arrivals, 64 lanes on a handful of counters, are worth the ballots.
+template <int kMinRun = 0>
 __device__ __forceinline__ uint32_t agg_add(uint32_t* ctr, uint32_t key, bool valid)
 {
   const uint32_t lane = __lane_id();
@@ -204,6 +209,7 @@ __device__ __forceinline__ uint32_t agg_add(uint32_t* ctr, uint32_t key, bool va
     const int leader = __ffsll((long long)active) - 1;
     const uint32_t k = __builtin_amdgcn_readlane(key, leader);
     const uint64_t peers = __ballot(valid && key == k) & active;
+    if(kMinRun > 0 && __popcll(peers) < kMinRun) break;
     uint32_t base = 0;
     if((int)lane == leader) base = atomicAdd(&ctr[k], (uint32_t)__popcll(peers));
     base = (uint32_t)__shfl((int)base, leader);
@@ -549,8 +555,8 @@ constexpr uint32_t kSortWork = 512 + kZoneWaves * 256;   // u32 of LDS the sort 
 __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t hi,
   uint32_t* s_work)
 {
-  uint32_t* s_bin = s_work;                // [2][256] running base of each digit (double-buffered)
-  uint32_t* s_wc = s_work + 512;           // [kZoneWaves][256] this tile's counts per wave
+  uint32_t* s_bin = s_work;                // [256] running base of each digit
+  uint32_t* s_wc = s_work + 512;           // [kZoneWaves][256] this tile's counts per wave -> bases
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint64_t* src = a;
@@ -582,54 +588,66 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
 #pragma unroll
       for(int k = 0; k < 4; ++k) { s_bin[lane * 4 + k] = run; run += v[k]; }
     }
-    uint32_t cb = 0;                       // which half of s_bin holds this tile's bases
-    // the items of kUnroll tiles are loaded together, then ranked tile by tile
-    uint64_t xs[kUnroll];
-    for(uint32_t t0 = 0; t0 < n; t0 += kZoneThreads)
+    // Tiles of kZoneThreads * kUnroll items; wave wv ranks the contiguous
+    // run [wv * 64 * kUnroll, +64 * kUnroll) of the tile, kUnroll rows of 64
+    // in order, keeping a running count per digit in s_wc[wv] — item order
+    // is (wave, row, lane), so the sort stays stable. Then, per digit, the
+    // waves' counts become their bases (prefix over waves on top of the
+    // running base s_bin) and every item goes to base + its rank. Three
+    // barriers per 4096 items (512-thread zones).
+    constexpr uint32_t kWaveItems = 64u * kUnroll;
+    for(uint32_t t0 = 0; t0 < n; t0 += kZoneThreads * kUnroll)
     {
-      const uint32_t tu = (t0 / kZoneThreads) % kUnroll;
-      if(tu == 0)
-      {
-#pragma unroll
-        for(int u = 0; u < kUnroll; ++u)
-        {
-          const uint32_t i = t0 + u * kZoneThreads + tid;
-          xs[u] = i < n ? src[i] : 0ull;
-        }
-      }
-      const uint32_t i = t0 + tid;
-      const bool valid = i < n;
-      uint64_t x = xs[0];
-#pragma unroll
-      for(int u = 1; u < kUnroll; ++u) x = tu == (uint32_t)u ? xs[u] : x;
-      const uint32_t d = (uint32_t)(x >> sh) & 255u;
-      // lanes of this wave holding the same digit: 8 ballots
-      uint64_t same = __ballot(valid);
-#pragma unroll
-      for(int bit = 0; bit < 8; ++bit)
-      {
-        const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
-        same &= ((d >> bit) & 1u) ? bb : ~bb;
-      }
       for(uint32_t k = lane; k < 256; k += 64) s_wc[wv * 256 + k] = 0;
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t rank = __popcll(same & lt);
-      if(valid && rank == 0) s_wc[wv * 256 + d] = __popcll(same);
-      lds_sync();                          // counts (and, first time, the bases) visible
-      if(valid)
+      uint64_t x[kUnroll];
+      const uint32_t wbase = t0 + wv * kWaveItems + lane;
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
       {
-        uint32_t pre = s_bin[cb * 256 + d];
-        for(uint32_t w = 0; w < wv; ++w) pre += s_wc[w * 256 + d];
-        dst[pre + rank] = x;
+        const uint32_t i = wbase + u * 64u;
+        x[u] = i < n ? src[i] : 0ull;
       }
+      __builtin_amdgcn_wave_barrier();
+      uint32_t rk[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const bool valid = wbase + u * 64u < n;
+        const uint32_t d = (uint32_t)(x[u] >> sh) & 255u;
+        // lanes of this row holding the same digit: 8 ballots
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for(int bit = 0; bit < 8; ++bit)
+        {
+          const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
+          same &= ((d >> bit) & 1u) ? bb : ~bb;
+        }
+        const uint32_t r = __popcll(same & lt);
+        const uint32_t c = s_wc[wv * 256 + d];   // this digit in the wave's earlier rows
+        rk[u] = c + r;
+        // (one wave: every lane's read above is done before this write)
+        __builtin_amdgcn_wave_barrier();
+        if(valid && r == 0) s_wc[wv * 256 + d] = c + (uint32_t)__popcll(same);
+        __builtin_amdgcn_wave_barrier();
+      }
+      lds_sync();                          // the waves' counts (and, first time, the bases) visible
       for(uint32_t k = tid; k < 256; k += kZoneThreads)
       {
-        uint32_t c = s_bin[cb * 256 + k];
-        for(uint32_t w = 0; w < (uint32_t)kZoneWaves; ++w) c += s_wc[w * 256 + k];
-        s_bin[(cb ^ 1u) * 256 + k] = c;
+        uint32_t run = s_bin[k];
+        for(uint32_t w = 0; w < (uint32_t)kZoneWaves; ++w)
+        {
+          const uint32_t c = s_wc[w * 256 + k];
+          s_wc[w * 256 + k] = run;
+          run += c;
+        }
+        s_bin[k] = run;
       }
-      cb ^= 1u;
-      lds_sync();                          // every read of s_wc and the old bases done
+      lds_sync();                          // per-wave bases visible
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+        if(wbase + u * 64u < n)
+          dst[s_wc[wv * 256 + ((uint32_t)(x[u] >> sh) & 255u)] + rk[u]] = x[u];
+      lds_sync();                          // every read of the bases done
     }
     // the pass's scattered stores are the next pass's loads (other threads)
     __syncthreads();
@@ -637,7 +655,22 @@ __device__ void coop_radix_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t l
   }
   if(src != a)
   {
-    for(uint32_t i = tid; i < n; i += kZoneThreads) a[i] = src[i];
+    for(uint32_t i0 = 0; i0 < n; i0 += kZoneThreads * kUnroll)
+    {
+      uint64_t x[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        x[u] = i < n ? src[i] : 0ull;
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        if(i < n) a[i] = x[u];
+      }
+    }
     __syncthreads();
   }
 }
@@ -728,9 +761,44 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
   }
   else
   {
-    for(uint32_t j = tid; j < g; j += kZoneThreads) tmp[j] = seg[(uint32_t)(ia[j] & pm)];
+    // kUnroll records in flight per thread in both passes
+    for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
+    {
+      uint32_t p[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        p[u] = j < g ? (uint32_t)(ia[j] & pm) : 0u;
+      }
+      uint4 r[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+        if(j0 + u * kZoneThreads + tid < g) r[u] = *reinterpret_cast<const uint4*>(seg + p[u]);
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j < g) *reinterpret_cast<uint4*>(tmp + j) = r[u];
+      }
+    }
     __syncthreads();
-    for(uint32_t j = tid; j < g; j += kZoneThreads) seg[j] = tmp[j];
+    for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
+    {
+      uint4 r[kUnroll];
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j < g) r[u] = *reinterpret_cast<const uint4*>(tmp + j);
+      }
+#pragma unroll
+      for(int u = 0; u < kUnroll; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j < g) *reinterpret_cast<uint4*>(seg + j) = r[u];
+      }
+    }
   }
   __syncthreads();
   return true;
@@ -772,6 +840,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
   __shared__ uint32_t s_tmp2[2 * kZoneWaves];
   __shared__ uint32_t s_nout;
+  __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
@@ -828,7 +897,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
   for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
-  if(tid == 0) { s_nout = 0; s_ntrig = 0; }
+  if(tid == 0) { s_nout = 0; s_ntrig = 0; s_nmix = 0; }
   __syncthreads();
   GPA_STAMP(0);
 
@@ -858,17 +927,41 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
   const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
   const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
-  // carried records counted apart (s_ccnt); landed ones in s_cnt
-  // carried mail is grouped by actor: a wave's lanes mostly share one
-  // counter (a backlog), folded into one atomic
-  for(uint32_t base = 0; base < nc; base += kZoneThreads * kUnroll)
+  // carried records counted apart (s_ccnt); landed ones in s_cnt.
+  // Carried mail is sorted by actor (carry-out writes each actor's remainder
+  // at its scan offset). A large carry (a backlog) is counted from samples:
+  // a run of kCarryRun records whose first and last belong to one actor is
+  // all that actor's, and only the runs that straddle actors are read whole
+  // (their positions listed in the index area, free until the place phase).
+  // Elsewhere a wave's lanes mostly share one counter, folded into one atomic.
+  uint32_t nmix = 0;
+  const uint32_t nrun = (nc + kCarryRun - 1) / kCarryRun;
+  const bool sampled = nc > kIdxCap && nrun <= kIdxCap / 2;     // uniform
+  uint32_t* const s_mix = reinterpret_cast<uint32_t*>(s_idx);
+  if(sampled)
+  {
+    for(uint32_t k = tid; k < nrun; k += kZoneThreads)
+    {
+      const uint32_t lo = k * kCarryRun, hi = min(lo + kCarryRun, nc);
+      const uint32_t a0 = C[lo].w0 & kZoneMask, a1 = C[hi - 1].w0 & kZoneMask;
+      if(a0 == a1)
+        atomicAdd(&s_ccnt[a0], hi - lo);
+      else
+        s_mix[atomicAdd(&s_nmix, 1u)] = k;
+    }
+    __syncthreads();
+    nmix = s_nmix;
+  }
+  const uint32_t ncount = sampled ? nmix * kCarryRun : nc;
+  for(uint32_t base = 0; base < ncount; base += kZoneThreads * kUnroll)
   {
     uint32_t w[kUnroll];
 #pragma unroll
     for(int u = 0; u < kUnroll; ++u)
     {
-      const uint32_t i = base + u * kZoneThreads + tid;
-      w[u] = i < nc ? C[i].w0 : 0xFFFFFFFFu;
+      const uint32_t j = base + u * kZoneThreads + tid;
+      const uint32_t i = sampled ? s_mix[min(j, ncount - 1) / kCarryRun] * kCarryRun + j % kCarryRun : j;
+      w[u] = (j < ncount && i < nc) ? C[i].w0 : 0xFFFFFFFFu;
     }
 #pragma unroll
     for(int u = 0; u < kUnroll; ++u)
@@ -905,9 +998,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t i = base + u * kZoneThreads + tid;
       w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
     }
+    // (a hot receiver's arrivals: lanes of one actor folded into one atomic)
 #pragma unroll
     for(int u = 0; u < kUnroll; ++u)
-      if(w[u] != 0xFFFFFFFFu) atomicAdd(&s_cnt[w[u] & kZoneMask], 1u);
+      (void)agg_add<8>(s_cnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
   }
   __syncthreads();
   GPA_STAMP(1);
@@ -1016,9 +1110,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
       {
-        if(r[u].x == 0xFFFFFFFFu) continue;
         const uint32_t a = r[u].x & kZoneMask;
-        pos[u] = s_off[a] + atomicAdd(&s_aux[a], 1u);
+        pos[u] = s_off[a] + agg_add<8>(s_aux, a, r[u].x != 0xFFFFFFFFu);
       }
 #pragma unroll
       for(int u = 0; u < kUnroll; ++u)
@@ -1222,20 +1315,49 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
       const uint32_t n = s_cnt[i];
       ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
-      // kUnroll records in flight per thread
-      for(uint32_t j0 = 0; j0 < rem; j0 += kZoneThreads * kUnroll)
+      if(c_eng.defer_big && !use_idx && co + rem <= cap)
       {
-        ZRec r[kUnroll];
+        // listed for k_carry_big, which copies it with every CU right after
+        // this launch (its sources, the carry buffer and S, stay untouched
+        // until then); a full list: copied here
+        if(tid == 0)
+        {
+          const uint32_t slot = atomicAdd(&c_eng.bigc_n[0], 1u);
+          uint32_t ok = 0;
+          if(slot < c_eng.bigc_cap)
+          {
+            BigCopy b;
+            b.c = C + s_cst[i]; b.p = Sz + s_off[i]; b.dst = cout + co;
+            b.ncc = s_ccnt[i]; b.from = n - rem; b.rem = rem; b.pad = 0;
+            c_eng.bigc[slot] = b;
+            ok = 1;
+          }
+          s_nmix = ok;
+        }
+        __syncthreads();
+        const bool listed = s_nmix != 0u;
+        __syncthreads();
+        if(listed) continue;
+      }
+      // Two half-batches of kUnroll / 2 records per thread, software-pipelined:
+      // one half's stores are issued behind the other half's loads, so waiting
+      // for a load never waits out the stores before it (vmcnt counts both,
+      // in issue order) and loads and stores stay in flight together.
+      constexpr int kH = kUnroll / 2;
+      constexpr uint32_t kStride = kZoneThreads * kH;
+      auto load_half = [&](ZRec (&r)[kH], uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
-        for(int uu = 0; uu < kUnroll; ++uu)
+        for(int uu = 0; uu < kH; ++uu)
         {
           const uint32_t j = j0 + uu * kZoneThreads + tid;
           if(j < rem)
             r[uu] = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
                             : AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}.rec(n - rem + j);
         }
+      };
+      auto store_half = [&](const ZRec (&r)[kH], uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
-        for(int uu = 0; uu < kUnroll; ++uu)
+        for(int uu = 0; uu < kH; ++uu)
         {
           const uint32_t j = j0 + uu * kZoneThreads + tid;
           if(j >= rem) continue;
@@ -1247,6 +1369,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           else
             spill_rec(nxt, kSpillCarry, z, pos, u);
         }
+      };
+      ZRec ra[kH], rb[kH];
+      load_half(ra, 0);
+      for(uint32_t j0 = 0; j0 < rem; j0 += 2 * kStride)
+      {
+        load_half(rb, j0 + kStride);
+        store_half(ra, j0);
+        load_half(ra, j0 + 2 * kStride);
+        store_half(rb, j0 + kStride);
       }
     }
   }

@@ -92,3 +92,21 @@ def test_priority(engine_factory, oracle, sources, sinks, bursts, m, batch, prio
           lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=16,
                            sink_priority=prio),
           W.fifo_result, mailbox_cap=16)
+
+
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("sources,sinks,bursts,m,batch", [
+    (100_000, 4, 2, 1, 100),    # four backlogs of ~25,000, drained 100 a step
+    (60_000, 40, 1, 1, 50),     # forty backlogs of 1,500 over one zone
+    (574_000, 4100, 1, 1, 5),   # 4,100 backlogs in one step: past the k_carry_big list
+])
+def test_backlog_copies(engine_factory, oracle, monkeypatch, defer, sources, sinks, bursts, m, batch):
+    """Backlogs (remainders above kBigGroup) copied to the next step's carry
+    by the zone's own workgroup (PONYC_AMD_DEFER_BIG=0) or listed for
+    k_carry_big and copied by every CU (1; past its 4,096-entry list the zone
+    copies the rest itself); carried backlogs are then counted from samples
+    (zone_dev.h kCarryRun). Bit-exact either way."""
+    monkeypatch.setenv("PONYC_AMD_DEFER_BIG", defer)
+    _both(engine_factory, oracle,
+          lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=16),
+          W.fifo_result, mailbox_cap=16)
