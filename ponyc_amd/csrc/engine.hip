@@ -519,6 +519,13 @@ int ensure_spill(uint64_t cap)
 
 int relayout_zones();
 int upload_types();
+int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out);
+
+// Spill list length for the current zone layout: a quarter of its records.
+inline uint64_t spill_cap_for_zones()
+{
+  return std::max<uint64_t>(1u << 20, g.zone_records / 4);
+}
 
 int read_sstat()
 {
@@ -590,10 +597,17 @@ int fixup_spill()
   HIPCK(hipStreamSynchronize(g.stream));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   g.fixups++;
-  // a list that overflowed lost records (counted as dropped): make it larger
-  if(most > g.spill_cap)
+  // Only now, with every spilled record placed, may the lists be re-sized
+  // (ensure_spill drops their contents): to the grown zones' share, and
+  // larger when a list overflowed (those records were counted as dropped).
+  // Re-sizing them inside relayout_zones, before k_spill_place had read them,
+  // lost every spilled record of a burst that grew the zones past 4 M records
+  // (round 3's 2048-sink backlog gap).
+  const uint64_t want = std::max<uint64_t>(spill_cap_for_zones(),
+                                           most > g.spill_cap ? 2ull * most : 0ull);
+  if(want > g.spill_cap)
   {
-    const int rc = ensure_spill(2ull * most);
+    const int rc = ensure_spill(want);
     if(rc) return rc;
     return upload_types();
   }
@@ -640,13 +654,29 @@ int relayout_zones()
 {
   // the geometry may change only before any step ran, with no mail landed
   // (zone buffers are copied zone by zone below)
+  // Every rank must pick the same geometry (the trigger-byte merge and the
+  // bucket layout assume it), so the choice follows the largest rank's share,
+  // ceil(n_actors / R), not this rank's own count, which can be one less; and
+  // whether mail has landed anywhere is summed over ranks (create is called
+  // by every rank alike, so this collective is reached by all of them).
   bool fresh = false;
   {
-    const uint32_t want = pick_zone_bits(g.n_local);
+    const uint32_t want = pick_zone_bits((g.n_actors + R() - 1) / R());
     if(want != g.zbits && g.steps_total == 0 && g.sparse_launches == 0)
     {
       HIPCK(hipStreamSynchronize(g.stream));
-      if(zones_empty())
+      bool empty = zones_empty();
+      if(R() > 1)
+      {
+        const unsigned long long mine = empty ? 0ull : 1ull;
+        HIPCK(hipMemcpyAsync(g.d_pend + kPendPre, &mine, sizeof(mine), hipMemcpyHostToDevice,
+          g.stream));
+        std::vector<unsigned long long> pv;
+        const int rc = pend_read(kPendPre, 1, pv);
+        if(rc) return rc;
+        empty = pv[0] == 0;
+      }
+      if(empty)
       {
         g.zbits = want;
         g.zcap_min.clear();
@@ -745,7 +775,9 @@ int relayout_zones()
     g.d_muted_on = mo;
     g.muted_on_cap = slots;
   }
-  return ensure_spill(std::max<uint64_t>(1u << 20, total / 4));
+  // (the spill lists are re-sized by the callers, once nothing is left in
+  // them: fixup_spill relays the zones while its spilled records wait there)
+  return 0;
 }
 
 uint32_t required_words(uint32_t ht)
@@ -1749,6 +1781,8 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   g.n_local = n_local;
   g.n_types = std::max(g.n_types, type_id + 1);
   int rc = relayout_zones();
+  if(rc) return rc;
+  rc = ensure_spill(spill_cap_for_zones());     // empty between calls: nothing to keep
   if(rc) return rc;
   rc = upload_types();
   if(rc) return rc;

@@ -52,6 +52,16 @@ CASES = {
     "xspill": (lambda e: W.ubench(e, 4096, 4, 32), W.ubench_result, {"max_exchange": 64}),
     "xspill_det": (lambda e: W.ubench(e, 3001, 3, det=True, hops=40), W.ubench_result,
                    {"max_exchange": 16}, "steps"),
+    # ~2048 FIFO sinks per rank taking 140 arrivals each, half of them from
+    # the other rank: every rank grows its sink zone 14x in one burst (and its
+    # spill lists after it), then drains 5 a step from backlogs of 135
+    "backlog": (lambda e: W.fifo(e, 4095 * 140, 4095, 1, 1, batch=5, mailbox_cap=16),
+                W.fifo_result, {"mailbox_cap": 16}),
+    # 2*2048*638 + 1 actors: rank 0 owns 639 zones' worth of 2048 and rank 1
+    # exactly 638, on either side of the 640-bucket geometry switch — both
+    # ranks must still pick the same zone size (engine.hip relayout_zones)
+    "zones_edge": (lambda e: W.ubench(e, 2 * 2048 * 638 + 1, 1, det=True, hops=3),
+                   W.ubench_result, {}),
 }
 
 

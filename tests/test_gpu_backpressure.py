@@ -98,11 +98,9 @@ def test_priority(engine_factory, oracle, sources, sinks, bursts, m, batch, prio
 @pytest.mark.parametrize("sources,sinks,bursts,m,batch", [
     (100_000, 4, 2, 1, 100),    # four backlogs of ~25,000, drained 100 a step
     (60_000, 40, 1, 1, 50),     # forty backlogs of 1,500 over one zone
-    pytest.param(574_000, 4100, 1, 1, 5, marks=pytest.mark.xfail(strict=True, reason=(
-        "known parity gap, same on the round-3 build before k_carry_big: a zone "
-        "of 2048 FIFO sinks taking 140 arrivals each (286,720 records into a "
-        "zone sized for 32,768) runs extra steps and ends in another order; "
-        "DESIGN.md §9"))),          # 4,100 backlogs in one step: past the k_carry_big list
+    (574_000, 4100, 1, 1, 5),   # 4,100 backlogs in one step: past the k_carry_big list
+    (410_000, 4100, 1, 1, 1000),  # two zones grown 9x in one burst, no carry
+    (2048 * 140, 2048, 1, 1, 5),  # one zone grown 14x: the spill lists re-sized after it
 ])
 def test_backlog_copies(engine_factory, oracle, monkeypatch, defer, sources, sinks, bursts, m, batch):
     """Backlogs (remainders above kBigGroup) copied to the next step's carry

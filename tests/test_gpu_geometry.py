@@ -33,6 +33,10 @@ CASES = {
     "fifo_hot": (lambda e: W.fifo(e, 4, 2, 1, 600, mailbox_cap=2048), W.fifo_result),
     "fifo_batch": (lambda e: W.fifo(e, 300, 3, 4, 9, batch=4, mailbox_cap=1), W.fifo_result),
     "spreader": (lambda e: W.spreader(e, 10), W.spreader_result),
+    # a zone of 4096 FIFO sinks grown 14x in one burst, then drained from
+    # backlogs of 135 (the spill lists re-sized only after the fixup placed them)
+    "backlog": (lambda e: W.fifo(e, 4096 * 140, 4096, 1, 1, batch=5, mailbox_cap=16),
+                W.fifo_result),
 }
 
 

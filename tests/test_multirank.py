@@ -41,7 +41,7 @@ def test_host_plumbing_gloo(nproc):
 @pytest.mark.parametrize("case", ["ring", "ring1", "ubench", "ubench_det", "fanin", "gups",
                                   "storm", "fifo", "fifo_seq", "spreader", "mute", "priority",
                                   "spill", "spill_one_rank", "spill_one_rank_fixed", "xspill",
-                                  "xspill_det"])
+                                  "xspill_det", "backlog", "zones_edge"])
 def test_two_ranks_one_gpu(case):
     out = _launch("mr_worker.py", 2, case)
     line = [l for l in out.splitlines() if l.startswith("MR_RESULT ")]
@@ -59,7 +59,7 @@ def test_two_ranks_one_gpu(case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["ubench_det", "storm", "spreader", "mute", "spill_one_rank",
-                                  "xspill"])
+                                  "xspill", "backlog"])
 def test_two_ranks_zones_4096(case, monkeypatch):
     """The same two-rank parity cases with 4096-actor zones forced
     (engine.hip: pick_zone_bits), as large engines run them."""
