@@ -26,8 +26,11 @@ Also reported on the same line:
                  KittyMac/ponyc src/libponyrt) running the same pinger graph
                  (oracle/_ref/harness_ubench) on this host: at every usable
                  physical core (--ponymaxthreads, SURVEY §8 d4, start.c:237-241)
-                 and at 1 thread, median of 5 runs each, same forward budget
-                 for both (rank 0, N=1);
+                 and at 1 thread; `value` is its steady state (pings handled
+                 in a window after warm-up, as message-ubench's report
+                 interval counts them), median of 3 runs each; `budgeted` is
+                 the same graph with a forward budget run to quiescence
+                 (median of 5) (rank 0, N=1);
   ring         — C1, examples/ring --size 1000 --count 100 --pass 10000 on
                  the GPU (run to quiescence, median of 3) beside the same
                  reference harness at the same core counts (BASELINE names
@@ -79,6 +82,9 @@ def parse():
     p.add_argument("--cpu-budget", type=int, default=10,
                    help="forward budget per pinger of the bounded CPU sample")
     p.add_argument("--cpu-runs", type=int, default=5)
+    p.add_argument("--cpu-steady-runs", type=int, default=3)
+    p.add_argument("--cpu-warm-ms", type=int, default=1000)
+    p.add_argument("--cpu-window-ms", type=int, default=2000)
     p.add_argument("--host-transport", action="store_true",
                    help="N > 1: exchange through pinned host memory + gloo instead of RCCL")
     return p.parse_args()
@@ -248,16 +254,52 @@ def cpu_reference(args, harness: str, hargs: dict, timeout: float) -> dict | Non
             "seconds_median_1thread": one["seconds_median"]}
 
 
+def cpu_steady(args, threads: int) -> dict:
+    """The reference runtime in steady state, as message-ubench measures it
+    (report interval, examples/message-ubench/main.pony:86-88, 288-299): no
+    forward budget; the pings handled in a window after a warm-up, ramp-down
+    to quiescence excluded. Median of args.cpu_steady_runs runs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    rates = []
+    for _ in range(args.cpu_steady_runs):
+        info, _ = pyoracle.run_harness("ubench", {
+            "pingers": args.actors, "initial": args.initial, "threads": threads, "noscale": 1,
+            "warm-ms": args.cpu_warm_ms, "window-ms": args.cpu_window_ms}, None, timeout=120)
+        rates.append(info["window_msgs_per_sec"])
+    return {"value": round(statistics.median(rates), 1), "runs": [round(r, 1) for r in rates]}
+
+
 def cpu_baseline(args) -> dict | None:
     r = cpu_reference(args, "ubench", {"pingers": args.actors, "initial": args.initial,
                                        "budget": args.cpu_budget}, timeout=300)
-    if r and r.get("value") is not None:
-        r["sample"] = (f"harness_ubench on KittyMac/ponyc libponyrt (-O3, pthread scaling): "
-                       f"{args.actors} pingers x {args.initial} initial pings, forward budget "
-                       f"{args.cpu_budget} per pinger ({r['msgs_per_run']} msgs per run), "
-                       f"--ponymaxthreads={r['cores']} (every usable physical core) and =1, "
-                       f"--ponynoblock --ponynoscale; median of {args.cpu_runs} runs each; "
-                       f"time = pony_start region (CLOCK_MONOTONIC)")
+    if not r or r.get("value") is None:
+        return r
+    budgeted = {"value": r.pop("value"), "value_1thread": r.pop("value_1thread"),
+                "runs": r.pop("runs"), "runs_1thread": r.pop("runs_1thread"),
+                "msgs_per_run": r.pop("msgs_per_run"),
+                "seconds_median": r.pop("seconds_median"),
+                "seconds_median_1thread": r.pop("seconds_median_1thread"),
+                "sample": (f"{args.actors} pingers x {args.initial} initial pings, forward "
+                           f"budget {args.cpu_budget} per pinger, run to quiescence (ramp-down "
+                           f"included); median of {args.cpu_runs} runs each; time = pony_start "
+                           f"region (CLOCK_MONOTONIC)")}
+    try:
+        allc = cpu_steady(args, r["cores"])
+        one = cpu_steady(args, 1)
+    except Exception as exc:         # report, never fake
+        r.update(value=None, sample=f"steady-state run failed: {exc!r}", budgeted=budgeted)
+        return r
+    r.update(value=allc["value"], value_1thread=one["value"], runs=allc["runs"],
+             runs_1thread=one["runs"], budgeted=budgeted)
+    r["sample"] = (f"harness_ubench on KittyMac/ponyc libponyrt (-O3, pthread scaling), steady "
+                   f"state: {args.actors} pingers x {args.initial} initial pings, no forward "
+                   f"budget; pings handled in a {args.cpu_window_ms} ms window after "
+                   f"{args.cpu_warm_ms} ms of warm-up (the reference's report interval, "
+                   f"message-ubench/main.pony:86-88, 288-299), then the pingers stop forwarding; "
+                   f"--ponymaxthreads={r['cores']} (every usable physical core) and =1, "
+                   f"--ponynoblock --ponynoscale; median of {args.cpu_steady_runs} runs each. "
+                   f"`budgeted`: the same graph with a forward budget, run to quiescence")
     return r
 
 

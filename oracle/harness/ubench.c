@@ -13,9 +13,20 @@
  * each pinger receives I initial pings. Usage:
  *   harness_ubench --pingers N --initial I [--budget B | --det 1 --hops H]
  *                  [--seed S] [--threads T] [--out file]
+ *                  [--warm-ms M --window-ms W]
  * Output (field-major u64): faithful: x, y, count; det: count, acc.
+ *
+ * Steady state (--window-ms W > 0, faithful form): no forward budget; as the
+ * reference's report interval does (main.pony:86-88, Tick 288-299), a timer
+ * thread lets the cascade run M ms, then counts the pings handled during
+ * the next W ms (sum of the pingers' counts read at both ends), then stops
+ * the pingers forwarding (Pinger.stop: _go = false, main.pony:257-259) so the
+ * runtime drains and pony_start returns. The JSON line then carries
+ * window_msgs_per_sec beside the whole-run figure.
  */
 #include "harness.h"
+#include <pthread.h>
+#include <unistd.h>
 
 enum { PING = 0 };
 
@@ -31,6 +42,10 @@ static pinger_t** g_ps;    /* _ps */
 static uint64_t g_n, g_budget, g_hops, g_seed;
 static int g_det;
 static uint64_t *g_x, *g_y, *g_count, *g_acc;
+static volatile int g_stop;        /* steady state: Pinger._go cleared */
+static uint64_t g_warm_ms, g_window_ms;
+static double g_win_secs;
+static uint64_t g_win_msgs;
 
 static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
 {
@@ -40,7 +55,7 @@ static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
   {
     /* be ping(payload): _count = _count + 1; send_pings() while in budget */
     p->count += 1;
-    if(p->count <= g_budget)
+    if(p->count <= g_budget && !g_stop)
     {
       uint64_t k = or_rand_int(&p->rand, g_n);         /* _rand.int(_num_ps) */
       pony_sendi(ctx, (pony_actor_t*)g_ps[k], PING, 42);
@@ -62,6 +77,30 @@ static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
 
 static pony_type_t pinger_type = { .id = 2, .size = sizeof(pinger_t), .dispatch = pinger_dispatch };
 
+/* pings handled so far: the pingers' counts, read while they run (each word
+ * is written by its own pinger; a read may be one ping stale) */
+static uint64_t count_sum(void)
+{
+  uint64_t s = 0;
+  for(uint64_t i = 0; i < g_n; i++) s += __atomic_load_n(&g_count[i], __ATOMIC_RELAXED);
+  return s;
+}
+
+static void* window_timer(void* arg)
+{
+  (void)arg;
+  usleep((useconds_t)(g_warm_ms * 1000));
+  double t0 = h_now();
+  uint64_t c0 = count_sum();
+  usleep((useconds_t)(g_window_ms * 1000));
+  double t1 = h_now();
+  uint64_t c1 = count_sum();
+  g_win_secs = t1 - t0;
+  g_win_msgs = c1 - c0;
+  g_stop = 1;
+  return NULL;
+}
+
 int main(int argc, char** argv)
 {
   g_n = h_arg(argc, argv, "--pingers", 8);
@@ -73,6 +112,9 @@ int main(int argc, char** argv)
   int threads = (int)h_arg(argc, argv, "--threads", 1);
   int noscale = (int)h_arg(argc, argv, "--noscale", 0);
   const char* out = h_sarg(argc, argv, "--out", "");
+  g_warm_ms = h_arg(argc, argv, "--warm-ms", 2000);
+  g_window_ms = h_arg(argc, argv, "--window-ms", 0);
+  if(g_window_ms && !g_det) g_budget = ~0ULL;
 
   g_ps = calloc(g_n, sizeof(pinger_t*));
   g_x = calloc(g_n, 8); g_y = calloc(g_n, 8); g_count = calloc(g_n, 8); g_acc = calloc(g_n, 8);
@@ -103,10 +145,25 @@ int main(int argc, char** argv)
       pony_sendi(ctx, (pony_actor_t*)g_ps[i], PING, (intptr_t)payload);
     }
 
+  pthread_t timer;
+  const int windowed = g_window_ms && !g_det;
+  if(windowed) pthread_create(&timer, NULL, window_timer, NULL);
   double secs = h_run(ctx);
+  if(windowed) pthread_join(timer, NULL);
 
   uint64_t total = 0;
   for(uint64_t i = 0; i < g_n; i++) total += g_count[i];
+  if(windowed)
+  {
+    printf("{\"harness\": \"ubench_steady\", \"threads\": %d, \"seconds\": %.6f, "
+      "\"msgs\": %llu, \"msgs_per_sec\": %.1f, \"warm_ms\": %llu, \"window_seconds\": %.6f, "
+      "\"window_msgs\": %llu, \"window_msgs_per_sec\": %.1f}\n", threads, secs,
+      (unsigned long long)total, secs > 0 ? (double)total / secs : 0.0,
+      (unsigned long long)g_warm_ms, g_win_secs, (unsigned long long)g_win_msgs,
+      g_win_secs > 0 ? (double)g_win_msgs / g_win_secs : 0.0);
+    fflush(stdout);
+    return 0;
+  }
   h_report(g_det ? "ubench_det" : "ubench", threads, secs, total);
   if(!g_det)
   {

@@ -59,6 +59,29 @@ def test_c2_ubench_steady_1m(engine_factory):
     assert int(st[2].max()) < 20 * steps
 
 
+def test_c2_ubench_steady_1m_vs_oracle(engine_factory, oracle):
+    """C2 exactly as bench.py runs it — 1,048,576 pingers x 5 pings, no
+    forward budget, a fixed number of supersteps — against the CPU
+    restatement: every pinger's xoroshiro128+ state [x, y] (KAT-pinned,
+    packages/random/_test.pony:473-493) and count bit for bit, and the
+    delivered / sent / pending counts."""
+    n, initial, steps = MILLION, 5, 8
+    e = engine_factory()
+    we = W.ubench(e, n, initial, budget=1 << 62)
+    e.run_fixed(steps)
+    ce = e.counts()
+    re = W.ubench_result(e, we)
+    wo = W.ubench(oracle, n, initial, budget=1 << 62)
+    oracle.run_fixed(steps)
+    co = oracle.counts()
+    ro = W.ubench_result(oracle, wo)
+    assert ce["dropped"] == 0
+    for k in ("delivered", "sent", "pending", "delivered_by_type"):
+        assert ce[k] == co[k], k
+    assert ce["delivered"] == steps * n * initial
+    np.testing.assert_array_equal(re, ro)
+
+
 def test_c3_fanin_100k(engine_factory, oracle):
     """C3: 100,000 senders -> 4 analyzers x 100 messages (atomic-enqueue
     contention worst case; analyzer counts and XOR folds bit-exact)."""
