@@ -493,6 +493,10 @@ int upload_types()
   g.defer_big = defer_big_wanted();
   e.bigc = g.d_bigc; e.bigc_n = g.d_bigc_n; e.bigc_cap = kBigCopyCap;
   e.defer_big = g.defer_big ? 1u : 0u;
+  {
+    const char* f = getenv("PONYC_AMD_TWO_PASS");
+    e.two_pass = (f && atoi(f) == 0) ? 0u : 1u;
+  }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -1271,7 +1275,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   const StepEntry se = pick_step_entry();
   if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
   // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
-  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(4 * (g.n_zones + (R() > 1 ? R() : 0)),
+  // (five for an order-free zone's two passes: zone_dev.h two_pass)
+  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(5 * (g.n_zones + (R() > 1 ? R() : 0)),
                                                           se.sort_work);
   step_kernel_t kern = se.kernel;
   if(e0)

@@ -191,6 +191,9 @@ struct EngDev {
   BigCopy* bigc;
   unsigned int* bigc_n;           // [2]: listed copies, finished k_carry_big workgroups
   uint32_t bigc_cap, defer_big;
+  // order-free zones run their behaviours twice instead of through the outbox
+  // (zone_dev.h two_pass; PONYC_AMD_TWO_PASS=0 turns it off for A/B runs)
+  uint32_t two_pass, pad7;
 };
 
 

@@ -818,6 +818,82 @@ __device__ __forceinline__ uint32_t zone_actor(const TypeDev& T, ZoneCtx& a, Acc
   return drain_zone<HT>(T, a, acc, n, nc, presorted);
 }
 
+// ---- order-free zones in two passes (no outbox) -------------------------------------
+// A zone of an order-free table whose mail all runs this step (k_step's `fast`
+// case) runs its behaviours twice instead of parking every send in the zone
+// outbox O and reading it back for the scatter: pass 1 (PlanCtx) only counts
+// the sends per (drain round, destination bucket) in LDS; one chunk per bucket
+// is reserved from the totals; pass 2 (TileCtx) runs the behaviours again on
+// the same register copy of each actor's state and puts every send straight at
+// its place in an LDS tile that is already sorted by bucket (the round's
+// counts give each bucket's start), and the tile leaves as runs of one chunk
+// each. The behaviours are deterministic functions of the state, so both
+// passes make the same sends. A drain round is one actor per thread.
+template <int HT> __host__ __device__ constexpr bool two_pass()
+{
+  return HT == GPU_ACTOR_HT_PINGER;     // order-free, at most one send per message
+}
+constexpr uint32_t kRounds = kZone / kZoneThreads;
+static_assert(kRounds == 4, "two rounds per packed count word, two words");
+// tile records after the per-actor counts at the head of the LDS pool
+constexpr uint32_t kPlanTile = kTile - kZone * sizeof(uint32_t) / sizeof(uint4);
+
+// Store record r = {to, w | src_local, arg lo, arg hi} at position pos of
+// bucket b's chunk: a destination zone's landing buffer (past its capacity:
+// the spill list), or a peer rank's exchange segment. Returns 1 if the
+// exchange lost it (its spill list full).
+__device__ __forceinline__ uint32_t emit_rec(const uint4& r, uint32_t b, uint32_t pos, uint32_t L0,
+  uint32_t nz, uint32_t nxt)
+{
+  const uint32_t from = (L0 + (r.y & kZoneMask)) * c_eng.nranks + c_eng.rank;
+  if(b < nz)
+  {
+    uint4 v;
+    v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
+    v.y = from;
+    v.z = r.z;
+    v.w = r.w;
+    if(pos < zone_capacity(b))
+      st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
+    else
+      spill_rec(nxt, 0u, b, pos, v);
+    return 0;
+  }
+  return xout_store(b - nz, pos, xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z));
+}
+
+// pass 1: count each send in its (round, bucket) — two rounds per u32 word,
+// 16 bits each (the zone's total is checked to fit)
+struct PlanCtx : ActorBase {
+  uint32_t* rh;
+  uint32_t inc;
+  __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg)
+  {
+    atomicAdd(&rh[bucket_of(to)], inc);
+  }
+};
+
+// pass 2: the send's rank in its bucket comes from the round's cursor; the
+// tile holds it at start + rank; past the tile it goes straight to its chunk
+struct TileCtx : ActorBase {
+  uint4* tile;
+  uint32_t* cur;          // [nb] bucket cursor in the tile (starts at the bucket's start)
+  const uint32_t* st;     // [nb] bucket start in the tile
+  const uint32_t* bs;     // [nb] next free position of the bucket's chunk
+  uint32_t L0, nz, nxt, xover;
+  __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg)
+  {
+    const uint32_t b = bucket_of(to);
+    const uint32_t idx = atomicAdd(&cur[b], 1u);
+    uint4 r;
+    r.x = to; r.y = w | src_local; r.z = (uint32_t)arg; r.w = (uint32_t)(arg >> 32);
+    if(idx < kPlanTile)
+      tile[idx] = r;
+    else
+      xover += emit_rec(r, b, bs[b] + (idx - st[b]), L0, nz, nxt);
+  }
+};
+
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
 // HTS >= 0: every serial actor of this engine runs handler table HTS (the host
 // checks), so only that table is compiled in; HTS < 0: any mix of tables.
@@ -841,6 +917,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_tmp2[2 * kZoneWaves];
   __shared__ uint32_t s_nout;
   __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
+  __shared__ uint32_t s_tot;                // messages pending in the zone (fast path)
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
@@ -897,7 +974,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
   for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
-  if(tid == 0) { s_nout = 0; s_ntrig = 0; s_nmix = 0; }
+  if(tid == 0) { s_nout = 0; s_ntrig = 0; s_nmix = 0; s_tot = 0; }
   __syncthreads();
   GPA_STAMP(0);
 
@@ -1028,14 +1105,28 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // every actor's mail fits its batch. Its records are
   // then never read — no segment scan, no index, no group sort. Otherwise
   // the zone takes the general path below.
-  bool fast = false;
+  bool fast = false, plan = false;
   if constexpr(HTS >= 0 && order_free<HTS>())
     if(!gate && ztc == 0 && tz >= 0)
     {
       const uint32_t bt = c_types[tz].prio ? 0xFFFFFFFFu : c_types[tz].batch;
       int over = 0;
-      for(uint32_t i = tid; i < kZone; i += kZoneThreads) over |= s_cnt[i] + s_ccnt[i] > bt;
+      uint32_t tot = 0;
+      for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+      {
+        const uint32_t c = s_cnt[i] + s_ccnt[i];
+        over |= c > bt;
+        tot += c;
+      }
+      tot = (uint32_t)min(wave_sum((unsigned long long)tot), 0xFFFFFFFFull);
+      if(lane == 0 && tot) atomicAdd(&s_tot, tot);
       fast = !__syncthreads_or(over);
+      // two passes when every (round, bucket) count fits 16 bits and no
+      // actor can run out of sequence numbers (pass 1 would count the
+      // overflow again): the zone's messages, each sending at most one, are
+      // fewer than seq_max
+      if constexpr(two_pass<HTS>())
+        plan = fast && s_tot < c_eng.seq_max && c_eng.two_pass != 0u;
     }
   ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
   if(fast)
@@ -1166,13 +1257,157 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   };
 
 
+  uint32_t delivered = 0, active = 0, sent = 0, applied = 0;
+  uint32_t n_atom = 0, dropped = 0, xover = 0;
+  uint32_t ncout = 0;
+  ZoneCtx a;
+  a.reset_common();
+  if constexpr(HTS >= 0 && two_pass<HTS>())
+    if(plan)
+    {
+      // ---- 3'. order-free zone: plan, reserve, emit (no outbox) -----------------------
+      constexpr int NW = HT_Words<HTS>::W;
+      const TypeDev T = c_types[tz];
+      uint32_t* const s_st = s_dyn;             // [nb] bucket totals, then the round's tile starts
+      uint32_t* const s_bs = s_dyn + nb;        // [nb] next free position of each chunk
+      uint32_t* const s_cur = s_dyn + 2 * nb;   // [nb] the round's tile cursors
+      uint32_t* const s_rh = s_dyn + 3 * nb;    // [2][nb] sends per (round, bucket), 16-bit halves
+      uint4* const tile = s_pool + kZone * sizeof(uint32_t) / sizeof(uint4);
+      for(uint32_t b = tid; b < 2 * nb; b += kZoneThreads) s_rh[b] = 0;
+      // every round's actor state, loaded at once (one memory round per thread)
+      uint64_t st[kRounds][NW];
+      uint32_t nm[kRounds];
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        const uint32_t i = r * kZoneThreads + tid;
+        nm[r] = i < nact ? s_cnt[i] : 0u;
+#pragma unroll
+        for(int k = 0; k < NW; ++k)
+          st[r][k] = nm[r] ? T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] : 0ull;
+      }
+      lds_sync();
+      // pass 1: count the sends of each round per bucket
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        if(!nm[r]) continue;
+        const uint32_t i = r * kZoneThreads + tid;
+        PlanCtx pc;
+        pc.reset_common();
+        pc.li = L0 + i - T.lfirst;
+        pc.self = (L0 + i) * R + me;
+        pc.src_local = i;
+        pc.type = tz;
+        pc.rh = s_rh + (r >> 1) * nb;
+        pc.inc = (r & 1u) ? 0x10000u : 1u;
+        uint64_t sc[NW];
+#pragma unroll
+        for(int k = 0; k < NW; ++k) sc[k] = st[r][k];
+        for(uint32_t j = 0; j < nm[r]; ++j) handle(HtTag<HTS>{}, T, pc, sc, 0u, 0ull);
+      }
+      lds_sync();
+      // one chunk per bucket for the zone's sends
+      for(uint32_t b = tid; b < nb; b += kZoneThreads)
+      {
+        const uint32_t w0 = s_rh[b], w1 = s_rh[nb + b];
+        const uint32_t h = (w0 & 0xFFFFu) + (w0 >> 16) + (w1 & 0xFFFFu) + (w1 >> 16);
+        uint32_t base = 0;
+        if(h)
+        {
+          ++n_atom;
+          if(b < nz)
+            base = atomicAdd(&c_eng.land_n[nxt][b], h);
+          else
+            base = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
+        }
+        s_bs[b] = base;
+      }
+      GPA_STAMP(5);
+      // pass 2, one round at a time
+      TileCtx tc;
+      tc.reset_common();
+      tc.tile = tile; tc.cur = s_cur; tc.st = s_st; tc.bs = s_bs;
+      tc.L0 = L0; tc.nz = nz; tc.nxt = nxt; tc.xover = 0;
+      uint32_t dz = 0;
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        // the round's bucket starts in the tile: an exclusive scan of its
+        // counts, each thread a contiguous run of buckets
+        {
+          const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
+          const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
+          const uint32_t* rw = s_rh + (r >> 1) * nb;
+          const uint32_t sh = (r & 1u) * 16u;
+          uint32_t sum = 0;
+          for(uint32_t b = lo; b < hi; ++b) sum += (rw[b] >> sh) & 0xFFFFu;
+          const uint32_t incl = wave_incl_scan(sum, lane);
+          if(lane == 63) s_tmp[wv] = incl;
+          lds_sync();
+          if(wv == 0)
+          {
+            uint32_t x = lane < (uint32_t)kZoneWaves ? s_tmp[lane] : 0u;
+            x = wave_incl_scan(x, lane);
+            if(lane < (uint32_t)kZoneWaves) s_tmp[lane] = x;
+          }
+          lds_sync();
+          uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
+          for(uint32_t b = lo; b < hi; ++b)
+          {
+            s_st[b] = run;
+            s_cur[b] = run;
+            run += (rw[b] >> sh) & 0xFFFFu;
+          }
+        }
+        const uint32_t tr = s_tmp[kZoneWaves - 1];     // the round's sends
+        lds_sync();
+        if(nm[r])
+        {
+          const uint32_t i = r * kZoneThreads + tid;
+          const uint32_t L = L0 + i;
+          tc.li = L - T.lfirst;
+          tc.self = L * R + me;
+          tc.src_local = i;
+          tc.type = tz;
+          tc.seq = 0;
+          for(uint32_t j = 0; j < nm[r]; ++j) handle(HtTag<HTS>{}, T, tc, st[r], 0u, 0ull);
+#pragma unroll
+          for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + tc.li] = st[r][k];
+          // overloaded iff a full batch ran (batch_limit_reached, actor.c:369-381);
+          // nothing here mutes
+          const bool full = T.prio ? (nm[r] % T.batch == 0u) : nm[r] == T.batch;
+          s_tb[i] = full ? 1u : 0u;
+          if(full) atomicAdd(&s_ntrig, 1u);
+          delivered += nm[r];
+          active += 1;
+          dz += nm[r];
+        }
+        lds_sync();
+        // the tile, sorted by bucket, to the chunks: runs of one chunk per wave store
+        const uint32_t m = min(tr, kPlanTile);
+        for(uint32_t q = tid; q < m; q += kZoneThreads)
+        {
+          const uint4 rec = tile[q];
+          const uint32_t b = bucket_of(rec.x);
+          xover += emit_rec(rec, b, s_bs[b] + (q - s_st[b]), L0, nz, nxt);
+        }
+        lds_sync();
+        // the chunks' next free positions
+        for(uint32_t b = tid; b < nb; b += kZoneThreads)
+          s_bs[b] += (s_rh[(r >> 1) * nb + b] >> ((r & 1u) * 16u)) & 0xFFFFu;
+      }
+      sent = tc.sent;
+      xover += tc.xover;
+      if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
+    }
+  if(!plan)
+  {
   // s_aux will hold each actor's unhandled remainder (known after it ran)
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   int any_rem = 0;
 
   // ---- 3. run handlers -------------------------------------------------------------
-  ZoneCtx a;
-  a.reset_common();
   a.out = c_eng.O + c_eng.zoff[z];
   a.s_nout = &s_nout;
   a.ocap = cap;
@@ -1186,7 +1421,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       a.fan_t = type_of_global((uint32_t)c_types[tz].params[1]);
       if(a.fan_t >= 0) a.fan = s_fan;
     }
-  uint32_t delivered = 0, active = 0, sent = 0, applied = 0, seqov = 0;
   // drain local actor i, of type t (T = c_types[t])
   uint8_t* const trig_cur = gate ? c_eng.trig[cur] : nullptr;
   auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
@@ -1283,7 +1517,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     atomicAdd(&s_bytype[a.applied_type], (unsigned long long)applied);
   // ---- 3b. carry-out: every actor's unhandled remainder, canonical, to the
   //      next step's carry buffer (none in the usual step) -----------------------------
-  uint32_t ncout = 0;
   if(__syncthreads_or(any_rem))
   {
     ncout = block_scan_zone(s_aux, s_tmp);
@@ -1381,6 +1614,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
     }
   }
+  }   // !plan
   if(tid == 0) c_eng.carry_n[nxt][z] = ncout;   // past cap: the tail is in the spill list
   // trigger bytes for the next step (only where some are set, or were)
   const uint32_t ntrig = s_ntrig;
@@ -1418,9 +1652,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
+  if(!plan)
+  {
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
-  uint32_t n_atom = 0;
   for(uint32_t b = tid; b < nb; b += kZoneThreads)
   {
     const uint32_t h = s_hist[b];
@@ -1442,24 +1677,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // scripts/ubench_scatter.hip).
   const uint32_t nout = min(s_nout, cap);
   const ORec* Oz = c_eng.O + c_eng.zoff[z];
-  uint32_t dropped = 0, xover = 0;
   // r = {to, w, arg lo, arg hi} -> position pos of bucket b's chunk
   auto emit = [&](const uint4& r, uint32_t b, uint32_t pos) __attribute__((always_inline)) {
-    const uint32_t from = (L0 + (r.y & kZoneMask)) * R + me;
-    if(b < nz)
-    {
-      uint4 v;
-      v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
-      v.y = from;
-      v.z = r.z;
-      v.w = r.w;
-      if(pos < zone_capacity(b))
-        st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
-      else
-        spill_rec(nxt, 0u, b, pos, v);
-    }
-    else
-      xover += xout_store(b - nz, pos, xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z));
+    xover += emit_rec(r, b, pos, L0, nz, nxt);
   };
   if(nout <= kZoneThreads)
   {
@@ -1522,6 +1742,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
     lds_sync();
   }
+  }   // !plan
 
   // ---- counters: block reduction, one atomic per workgroup per counter ---------------
   unsigned long long v[6] = { delivered + applied, sent, active, dropped, xover, n_atom };
