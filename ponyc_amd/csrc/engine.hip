@@ -198,35 +198,55 @@ __global__ void __launch_bounds__(kBlock) k_spill_place(const SpillRec* s, uint3
   base[c_eng.zoff[r.z] + (r.tag & kSpillPosMask)] = r.rec;
 }
 
-// Backlog copies listed by k_step (EngDev::bigc, defer_big): every workgroup
-// takes its stride of every listed copy, so one overloaded receiver's
-// remainder moves at the whole GPU's bandwidth instead of one CU's; the last
-// workgroup to finish clears the list for the next step.
+// Backlog copies listed by k_step (EngDev::bigc, defer_big): the listed
+// records form one flat range (each copy's base, in slot order), cut into
+// equal contiguous chunks, one per workgroup; a workgroup finds the first copy
+// its chunk touches (binary search over the bases) and walks on from there,
+// so one overloaded receiver's remainder moves at the whole GPU's bandwidth
+// and no workgroup visits copies outside its chunk. With nothing listed the
+// kernel returns at once; otherwise the last workgroup to finish clears the
+// list for the next step.
 constexpr uint32_t kBigCopyCap = 4096;
 constexpr uint32_t kBigCopyBlocks = 512;
 __global__ void __launch_bounds__(kBlock) k_carry_big()
 {
-  const uint32_t n = min(c_eng.bigc_n[0], c_eng.bigc_cap);
-  const uint32_t stride = gridDim.x * kBlock;
-  for(uint32_t d = 0; d < n; ++d)
+  const unsigned long long v = c_eng.bigc_n[0];   // final: k_step ran to completion before
+  const uint32_t n = min((uint32_t)(v >> 32), c_eng.bigc_cap);
+  if(n == 0) return;
+  const uint32_t total = (uint32_t)v;
+  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * per, c1 = min(c0 + per, total);
+  if(c0 < c1)
   {
-    const BigCopy b = c_eng.bigc[d];
-    for(uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < b.rem; j += stride)
+    uint32_t lo = 0, hi = n - 1;                   // last copy with base <= c0
+    while(lo < hi)
     {
-      const uint32_t k = b.from + j;
-      const uint4 r = k < b.ncc ? *reinterpret_cast<const uint4*>(b.c + k)
-                                : *reinterpret_cast<const uint4*>(b.p + (k - b.ncc));
-      *reinterpret_cast<uint4*>(b.dst + j) = r;
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if(c_eng.bigc[mid].base <= c0) lo = mid; else hi = mid - 1;
+    }
+    for(uint32_t d = lo; d < n; ++d)
+    {
+      const BigCopy b = c_eng.bigc[d];
+      if(b.base >= c1) break;
+      const uint32_t j0 = c0 > b.base ? c0 - b.base : 0u;       // b.base < c1 here
+      const uint32_t j1 = min(c1 - b.base, b.rem);
+      for(uint32_t j = j0 + threadIdx.x; j < j1; j += kBlock)
+      {
+        const uint32_t k = b.from + j;
+        const uint4 r = k < b.ncc ? *reinterpret_cast<const uint4*>(b.c + k)
+                                  : *reinterpret_cast<const uint4*>(b.p + (k - b.ncc));
+        *reinterpret_cast<uint4*>(b.dst + j) = r;
+      }
     }
   }
   __syncthreads();
   if(threadIdx.x == 0)
   {
     __threadfence();
-    if(atomicAdd(&c_eng.bigc_n[1], 1u) == gridDim.x - 1)
+    if(atomicAdd(&c_eng.bigc_n[1], 1ull) == gridDim.x - 1)
     {
-      atomicExch(&c_eng.bigc_n[0], 0u);
-      atomicExch(&c_eng.bigc_n[1], 0u);
+      atomicExch(&c_eng.bigc_n[0], 0ull);
+      atomicExch(&c_eng.bigc_n[1], 0ull);
     }
   }
 }
@@ -319,8 +339,10 @@ struct Engine {
   gpu_actor_alltoallv_fn xp_a2a = nullptr;
   gpu_actor_allreduce_fn xp_ar = nullptr;
   void* xp_ctx = nullptr;
-  XRec* h_xout = nullptr;
-  XRec* h_xin = nullptr;
+  // host transport staging (pinned): what this rank sends, what it receives
+  uint8_t* h_sbuf = nullptr;
+  uint8_t* h_rbuf = nullptr;
+  uint64_t h_sbuf_cap = 0, h_rbuf_cap = 0;
   // spawned actors (gpu_actor_type_reserve)
   uint32_t spawn_cap = 0;
   uint64_t *d_skey[2] = {nullptr, nullptr}, *d_sarg[2] = {nullptr, nullptr};
@@ -352,7 +374,7 @@ struct Engine {
   uint32_t sidx = 0;
   // backlog copies handed to k_carry_big (EngDev::bigc)
   BigCopy* d_bigc = nullptr;
-  unsigned int* d_bigc_n = nullptr;
+  unsigned long long* d_bigc_n = nullptr;
   bool defer_big = false;
   SpillRec* d_spill[2] = {nullptr, nullptr};
   uint32_t spill_cap = 0;
@@ -888,12 +910,6 @@ int exchange_room(uint64_t max_send, uint64_t total_recv, uint64_t xs)
     HIPCK(hipStreamSynchronize(g.stream));
     HIPCK(hipFree(g.d_xout));
     g.d_xout = nx;
-    if(g.xp_a2a)
-    {
-      HIPCK(hipHostFree(g.h_xout));
-      g.h_xout = nullptr;
-      HIPCK(hipHostMalloc(&g.h_xout, (size_t)R() * cap * sizeof(XRec), hipHostMallocDefault));
-    }
     g.xcap = (uint32_t)cap;
     const int rc = upload_types();
     if(rc) return rc;
@@ -925,14 +941,173 @@ int exchange_room(uint64_t max_send, uint64_t total_recv, uint64_t xs)
     HIPCK(hipFree(g.d_xin));
     g.d_xin = nullptr;
     HIPCK(hipMalloc(&g.d_xin, cap * sizeof(XRec)));
-    if(g.xp_a2a)
-    {
-      HIPCK(hipHostFree(g.h_xin));
-      g.h_xin = nullptr;
-      HIPCK(hipHostMalloc(&g.h_xin, cap * sizeof(XRec), hipHostMallocDefault));
-    }
     g.xin_cap = cap;
   }
+  return 0;
+}
+
+// ---- cross-rank collectives on device buffers ---------------------
+// Every cross-rank step of the engine — the exchange's counts and records,
+// the trigger-byte and spill-flag merges, the spawn gather, the pending and
+// counter sums — calls only these four, on device buffers in stream order.
+// Each has two implementations: RCCL on the engine's stream (ncclAllReduce /
+// ncclAllToAll / ncclAllGather / grouped ncclSend+ncclRecv over xGMI), and
+// the host transport (gpu_actor_set_transport: the same device buffers
+// staged through pinned host memory and the two callbacks). The control flow
+// around them is one path, so the host-transport tests run it all; only the
+// nccl* calls inside these functions are left to the RCCL runs.
+enum XcType { XC_U8 = 0, XC_U32 = 1, XC_U64 = 2 };
+
+int stage_room(uint64_t sbytes, uint64_t rbytes)
+{
+  if(sbytes > g.h_sbuf_cap)
+  {
+    if(g.h_sbuf) HIPCK(hipHostFree(g.h_sbuf));
+    g.h_sbuf = nullptr;
+    const uint64_t c = std::max<uint64_t>(sbytes, 2 * g.h_sbuf_cap);
+    HIPCK(hipHostMalloc(&g.h_sbuf, c, hipHostMallocDefault));
+    g.h_sbuf_cap = c;
+  }
+  if(rbytes > g.h_rbuf_cap)
+  {
+    if(g.h_rbuf) HIPCK(hipHostFree(g.h_rbuf));
+    g.h_rbuf = nullptr;
+    const uint64_t c = std::max<uint64_t>(rbytes, 2 * g.h_rbuf_cap);
+    HIPCK(hipHostMalloc(&g.h_rbuf, c, hipHostMallocDefault));
+    g.h_rbuf_cap = c;
+  }
+  return 0;
+}
+
+// d_out[i] = Σ over ranks of d_in[i], i < count (in place when d_in == d_out).
+// XC_U8 on the host transport sums 8 bytes per word: every byte must have
+// one nonzero contributor (the trigger bytes: each rank writes its own ids).
+int xc_allreduce_sum(const void* d_in, void* d_out, uint64_t count, XcType t)
+{
+  if(count == 0) return 0;
+  if(!g.xp_ar)
+  {
+    const ncclDataType_t nt = t == XC_U8 ? ncclUint8 : t == XC_U32 ? ncclUint32 : ncclUint64;
+    NCCLCK(ncclAllReduce(d_in, d_out, count, nt, ncclSum, g.comm, g.stream));
+    return 0;
+  }
+  const uint64_t esz = t == XC_U8 ? 1 : t == XC_U32 ? 4 : 8;
+  const uint64_t bytes = count * esz;
+  const uint64_t words = t == XC_U64 ? count : t == XC_U8 ? (bytes + 7) / 8 : count;
+  int rc = stage_room(words * 8, bytes);
+  if(rc) return rc;
+  uint64_t* w = reinterpret_cast<uint64_t*>(g.h_sbuf);
+  if(t == XC_U8) memset(w, 0, words * 8);
+  HIPCK(hipMemcpyAsync(t == XC_U32 ? g.h_rbuf : g.h_sbuf, d_in, bytes, hipMemcpyDeviceToHost,
+    g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  if(t == XC_U32)
+    for(uint64_t i = 0; i < count; ++i) w[i] = reinterpret_cast<const uint32_t*>(g.h_rbuf)[i];
+  if(g.xp_ar(g.xp_ctx, w, words) != 0) return GPU_ACTOR_ECOMM;
+  if(t == XC_U32)
+  {
+    for(uint64_t i = 0; i < count; ++i)
+      reinterpret_cast<uint32_t*>(g.h_rbuf)[i] = (uint32_t)std::min<uint64_t>(w[i], 0xFFFFFFFFull);
+    HIPCK(hipMemcpyAsync(d_out, g.h_rbuf, bytes, hipMemcpyHostToDevice, g.stream));
+  }
+  else
+    HIPCK(hipMemcpyAsync(d_out, g.h_sbuf, bytes, hipMemcpyHostToDevice, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));       // the staging is reused by the next call
+  return 0;
+}
+
+// d_recv[p] = peer p's d_send[rank] (one u64 per peer).
+int xc_alltoall_u64(const unsigned long long* d_send, unsigned long long* d_recv)
+{
+  const uint32_t n = R();
+  if(!g.xp_a2a)
+  {
+    NCCLCK(ncclAllToAll(d_send, d_recv, 1, ncclUint64, g.comm, g.stream));
+    return 0;
+  }
+  int rc = stage_room(n * 8, n * 8);
+  if(rc) return rc;
+  HIPCK(hipMemcpyAsync(g.h_sbuf, d_send, n * 8, hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  std::vector<uint64_t> b8(n, 8);
+  if(g.xp_a2a(g.xp_ctx, g.h_sbuf, b8.data(), g.h_rbuf, b8.data()) != 0) return GPU_ACTOR_ECOMM;
+  HIPCK(hipMemcpyAsync(d_recv, g.h_rbuf, n * 8, hipMemcpyHostToDevice, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  return 0;
+}
+
+// d_out[p] = rank p's d_in[0] (one u64 per rank).
+int xc_allgather_u64(const unsigned long long* d_in, unsigned long long* d_out)
+{
+  const uint32_t n = R();
+  if(!g.xp_a2a)
+  {
+    NCCLCK(ncclAllGather(d_in, d_out, 1, ncclUint64, g.comm, g.stream));
+    return 0;
+  }
+  int rc = stage_room(n * 8, n * 8);
+  if(rc) return rc;
+  HIPCK(hipMemcpyAsync(g.h_sbuf, d_in, 8, hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  uint64_t* sw = reinterpret_cast<uint64_t*>(g.h_sbuf);
+  for(uint32_t p = 1; p < n; ++p) sw[p] = sw[0];
+  std::vector<uint64_t> b8(n, 8);
+  if(g.xp_a2a(g.xp_ctx, g.h_sbuf, b8.data(), g.h_rbuf, b8.data()) != 0) return GPU_ACTOR_ECOMM;
+  HIPCK(hipMemcpyAsync(d_out, g.h_rbuf, n * 8, hipMemcpyHostToDevice, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  return 0;
+}
+
+// One grouped exchange: to each peer p != rank, send[p] bytes from d_send[p];
+// from it, recv[p] bytes into d_recv[p] (either may be 0).
+struct XcPeer {
+  const void* d_send = nullptr;
+  uint64_t send = 0;
+  void* d_recv = nullptr;
+  uint64_t recv = 0;
+};
+int xc_sendrecv(const std::vector<XcPeer>& pp)
+{
+  const uint32_t n = R();
+  if(!g.xp_a2a)
+  {
+    NCCLCK(ncclGroupStart());
+    for(uint32_t p = 0; p < n; ++p)
+    {
+      if(p == rank()) continue;
+      if(pp[p].send) NCCLCK(ncclSend(pp[p].d_send, pp[p].send, ncclUint8, p, g.comm, g.stream));
+      if(pp[p].recv) NCCLCK(ncclRecv(pp[p].d_recv, pp[p].recv, ncclUint8, p, g.comm, g.stream));
+    }
+    NCCLCK(ncclGroupEnd());
+    return 0;
+  }
+  std::vector<uint64_t> sb(n, 0), rb(n, 0);
+  uint64_t st = 0, rt = 0;
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    if(p == rank()) continue;
+    sb[p] = pp[p].send;
+    rb[p] = pp[p].recv;
+    st += sb[p];
+    rt += rb[p];
+  }
+  int rc = stage_room(std::max<uint64_t>(st, 8), std::max<uint64_t>(rt, 8));
+  if(rc) return rc;
+  uint64_t off = 0;
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    if(sb[p]) HIPCK(hipMemcpyAsync(g.h_sbuf + off, pp[p].d_send, sb[p], hipMemcpyDeviceToHost, g.stream));
+    off += sb[p];
+  }
+  HIPCK(hipStreamSynchronize(g.stream));
+  if(g.xp_a2a(g.xp_ctx, g.h_sbuf, sb.data(), g.h_rbuf, rb.data()) != 0) return GPU_ACTOR_ECOMM;
+  off = 0;
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    if(rb[p]) HIPCK(hipMemcpyAsync(pp[p].d_recv, g.h_rbuf + off, rb[p], hipMemcpyHostToDevice, g.stream));
+    off += rb[p];
+  }
+  HIPCK(hipStreamSynchronize(g.stream));
   return 0;
 }
 
@@ -952,95 +1127,50 @@ int exchange_step(uint32_t step_sidx)
   uint64_t total = 0;
   hipLaunchKernelGGL(k_xprep, dim3(1), dim3(64), 0, g.stream);
   HIPCK(hipGetLastError());
-  if(g.xp_a2a)
+  // send counts to every peer (device), the step's trigger count summed
+  int rc = xc_alltoall_u64(g.d_xcount, g.d_xrecv);
+  if(rc) return rc;
+  rc = xc_allreduce_sum(g.d_trig_n + tslot, g.d_trig_n + tslot, 1, XC_U32);
+  if(rc) return rc;
+  // the step's one readback: send and receive counts, trigger count, kept
+  // exchange-spill records, spill status
+  g.h_xc[2 * n] = 0;
+  g.h_xc[2 * n + 1] = 0;
+  HIPCK(hipMemcpyAsync(g.h_xc, g.d_xc, 2 * n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    g.stream));
+  HIPCK(hipMemcpyAsync(g.h_xc + 2 * n, g.d_trig_n + tslot, sizeof(unsigned int),
+    hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipMemcpyAsync(g.h_xc + 2 * n + 1, g.d_xspill_n, sizeof(unsigned int),
+    hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
+    g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  tcount = (unsigned int)(g.h_xc[2 * n] & 0xFFFFFFFFull);
+  const uint64_t xs = g.h_xc[2 * n + 1] & 0xFFFFFFFFull;
+  std::vector<uint64_t> roff(n);
+  uint64_t max_send = 0;
+  for(uint32_t p = 0; p < n; ++p)
   {
-    unsigned int tloc = 0, xs = 0;
-    HIPCK(hipMemcpyAsync(g.h_xc, g.d_xcount, n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-      g.stream));
-    HIPCK(hipMemcpyAsync(&tloc, g.d_trig_n + tslot, sizeof(tloc), hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipMemcpyAsync(&xs, g.d_xspill_n, sizeof(xs), hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
-      g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
-    std::vector<uint64_t> sc(n), cb(n, sizeof(uint64_t)), sb(n), rb(n), rcv(n, 0);
-    uint64_t max_send = 0;
-    for(uint32_t p = 0; p < n; ++p)
-    {
-      sc[p] = p == rank() ? 0 : g.h_xc[p];
-      max_send = std::max(max_send, sc[p]);
-    }
-    if(g.xp_a2a(g.xp_ctx, sc.data(), cb.data(), rcv.data(), cb.data()) != 0) return GPU_ACTOR_ECOMM;
-    uint64_t t64 = tloc;
-    if(g.xp_ar(g.xp_ctx, &t64, 1) != 0) return GPU_ACTOR_ECOMM;
-    tcount = (unsigned int)t64;
-    HIPCK(hipMemcpyAsync(g.d_trig_n + tslot, &tcount, sizeof(tcount), hipMemcpyHostToDevice,
-      g.stream));
-    uint64_t rtot = 0;
-    for(uint32_t p = 0; p < n; ++p) rtot += rcv[p];
-    int rc = exchange_room(max_send, rtot, xs);
-    if(rc) return rc;
-    uint64_t soff = 0;
-    for(uint32_t p = 0; p < n; ++p)
-    {
-      if(sc[p])
-        HIPCK(hipMemcpyAsync(g.h_xout + soff, g.d_xout + (size_t)p * g.xcap, sc[p] * sizeof(XRec),
-          hipMemcpyDeviceToHost, g.stream));
-      soff += sc[p];
-      total += rcv[p];
-      sb[p] = sc[p] * sizeof(XRec);
-      rb[p] = rcv[p] * sizeof(XRec);
-      g.h_xc[n + p] = rcv[p];
-    }
-    HIPCK(hipStreamSynchronize(g.stream));
-    if(g.xp_a2a(g.xp_ctx, g.h_xout, sb.data(), g.h_xin, rb.data()) != 0) return GPU_ACTOR_ECOMM;
-    if(total)
-      HIPCK(hipMemcpyAsync(g.d_xin, g.h_xin, total * sizeof(XRec), hipMemcpyHostToDevice, g.stream));
-    // per-peer counts for k_xinject (the sender's rank of each record)
-    HIPCK(hipMemcpyAsync(g.d_xrecv, g.h_xc + n, n * sizeof(unsigned long long),
-      hipMemcpyHostToDevice, g.stream));
+    roff[p] = total;
+    if(p == rank()) continue;
+    total += g.h_xc[n + p];
+    max_send = std::max<uint64_t>(max_send, g.h_xc[p]);
   }
-  else
+  rc = exchange_room(max_send, total, xs);
+  if(rc) return rc;
+  // the records: each peer's segment of xout to it, its records into xin in
+  // rank order (k_xinject tells the sender of a record by its segment)
+  std::vector<XcPeer> pp(n);
+  for(uint32_t p = 0; p < n; ++p)
   {
-    NCCLCK(ncclAllToAll(g.d_xcount, g.d_xrecv, 1, ncclUint64, g.comm, g.stream));
-    NCCLCK(ncclAllReduce(g.d_trig_n + tslot, g.d_trig_n + tslot, 1, ncclUint32, ncclSum, g.comm,
-      g.stream));
-    g.h_xc[2 * n] = 0;
-    g.h_xc[2 * n + 1] = 0;
-    HIPCK(hipMemcpyAsync(g.h_xc, g.d_xc, 2 * n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-      g.stream));
-    HIPCK(hipMemcpyAsync(g.h_xc + 2 * n, g.d_trig_n + tslot, sizeof(unsigned int),
-      hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipMemcpyAsync(g.h_xc + 2 * n + 1, g.d_xspill_n, sizeof(unsigned int),
-      hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
-      g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));            // the step's one synchronisation
-    tcount = (unsigned int)(g.h_xc[2 * n] & 0xFFFFFFFFull);
-    const uint64_t xs = g.h_xc[2 * n + 1] & 0xFFFFFFFFull;
-    std::vector<uint64_t> roff(n);
-    uint64_t max_send = 0;
-    for(uint32_t p = 0; p < n; ++p)
-    {
-      roff[p] = total;
-      if(p == rank()) continue;
-      total += g.h_xc[n + p];
-      max_send = std::max<uint64_t>(max_send, g.h_xc[p]);
-    }
-    int rc = exchange_room(max_send, total, xs);
-    if(rc) return rc;
-    NCCLCK(ncclGroupStart());
-    for(uint32_t p = 0; p < n; ++p)
-    {
-      if(p == rank()) continue;
-      const uint64_t sc = g.h_xc[p];
-      const uint64_t rcn = g.h_xc[n + p];
-      if(sc) NCCLCK(ncclSend(g.d_xout + (size_t)p * g.xcap, sc * sizeof(XRec), ncclUint8, p,
-        g.comm, g.stream));
-      if(rcn) NCCLCK(ncclRecv(g.d_xin + roff[p], rcn * sizeof(XRec), ncclUint8, p, g.comm,
-        g.stream));
-    }
-    NCCLCK(ncclGroupEnd());
+    if(p == rank()) continue;
+    pp[p].d_send = g.d_xout + (size_t)p * g.xcap;
+    pp[p].send = g.h_xc[p] * sizeof(XRec);
+    pp[p].d_recv = g.d_xin + roff[p];
+    pp[p].recv = g.h_xc[n + p] * sizeof(XRec);
   }
+  rc = xc_sendrecv(pp);
+  if(rc) return rc;
   g.remote_total += total;
   if(total)
   {
@@ -1053,39 +1183,14 @@ int exchange_step(uint32_t step_sidx)
   // byte has one writer, so the sum is the merge), over the ids in use only
   if(tcount || g.trig_stale[land_par])
   {
-    const uint64_t tb = trig_live_bytes();
-    if(g.xp_ar)
-    {
-      std::vector<uint64_t> h(tb / 8);
-      HIPCK(hipMemcpyAsync(h.data(), g.d_trig_own[land_par], tb, hipMemcpyDeviceToHost,
-        g.stream));
-      HIPCK(hipStreamSynchronize(g.stream));
-      if(g.xp_ar(g.xp_ctx, h.data(), h.size()) != 0) return GPU_ACTOR_ECOMM;
-      HIPCK(hipMemcpyAsync(g.d_trig[land_par], h.data(), tb, hipMemcpyHostToDevice,
-        g.stream));
-      HIPCK(hipStreamSynchronize(g.stream));
-    }
-    else
-      NCCLCK(ncclAllReduce(g.d_trig_own[land_par], g.d_trig[land_par], tb, ncclUint8,
-        ncclSum, g.comm, g.stream));
+    rc = xc_allreduce_sum(g.d_trig_own[land_par], g.d_trig[land_par], trig_live_bytes(), XC_U8);
+    if(rc) return rc;
   }
   g.trig_stale[land_par] = tcount != 0;
   // did any rank's zone overflow (this step or its landing)? summed on device
   hipLaunchKernelGGL(k_spill_flag, dim3(1), dim3(1), 0, g.stream, g.d_spill_flag);
   HIPCK(hipGetLastError());
-  if(g.xp_ar)
-  {
-    unsigned int f = 0;
-    HIPCK(hipMemcpyAsync(&f, g.d_spill_flag, sizeof(f), hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
-    uint64_t f64 = f;
-    if(g.xp_ar(g.xp_ctx, &f64, 1) != 0) return GPU_ACTOR_ECOMM;
-    f = (unsigned int)std::min<uint64_t>(f64, 0xFFFFFFFFull);
-    HIPCK(hipMemcpyAsync(g.d_spill_flag, &f, sizeof(f), hipMemcpyHostToDevice, g.stream));
-  }
-  else
-    NCCLCK(ncclAllReduce(g.d_spill_flag, g.d_spill_flag, 1, ncclUint32, ncclSum, g.comm, g.stream));
-  return 0;
+  return xc_allreduce_sum(g.d_spill_flag, g.d_spill_flag, 1, XC_U32);
 }
 
 // k_step compiled for the one handler table all serial actors share, when
@@ -1140,20 +1245,14 @@ int spawn_process(uint32_t cur)
   {
     const uint32_t nr = R();
     std::vector<uint64_t> cnt(nr, 0);
-    if(g.xp_a2a)
-    {
-      std::vector<uint64_t> mine(nr, n), b8(nr, sizeof(uint64_t));
-      if(g.xp_a2a(g.xp_ctx, mine.data(), b8.data(), cnt.data(), b8.data()) != 0)
-        return GPU_ACTOR_ECOMM;
-    }
-    else
     {
       unsigned long long* dc = g.d_xc + 2 * nr;     // scratch words of the counts block
       const unsigned long long mine = n;
       HIPCK(hipMemcpyAsync(dc, &mine, sizeof(mine), hipMemcpyHostToDevice, g.stream));
       unsigned long long* dall = nullptr;
       HIPCK(hipMalloc(&dall, nr * sizeof(unsigned long long)));
-      NCCLCK(ncclAllGather(dc, dall, 1, ncclUint64, g.comm, g.stream));
+      int rc = xc_allgather_u64(dc, dall);
+      if(rc) { (void)hipFree(dall); return rc; }
       HIPCK(hipMemcpyAsync(cnt.data(), dall, nr * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
       HIPCK(hipStreamSynchronize(g.stream));
       HIPCK(hipFree(dall));
@@ -1182,59 +1281,22 @@ int spawn_process(uint32_t cur)
       HIPCK(hipMemcpyAsync(g.d_sarg[1] + off[rank()], g.d_sarg[0], n * sizeof(uint64_t),
         hipMemcpyDeviceToDevice, g.stream));
     }
-    if(g.xp_a2a)
+    // every peer gets our n records; we get each peer's (keys, then args)
+    for(int part = 0; part < 2; ++part)
     {
-      std::vector<uint64_t> hk(total), ha(total), sb(nr), rb(nr);
-      std::vector<uint64_t> lk(n), la(n);
-      if(n)
-      {
-        HIPCK(hipMemcpyAsync(lk.data(), g.d_skey[0], n * sizeof(uint64_t), hipMemcpyDeviceToHost,
-          g.stream));
-        HIPCK(hipMemcpyAsync(la.data(), g.d_sarg[0], n * sizeof(uint64_t), hipMemcpyDeviceToHost,
-          g.stream));
-      }
-      HIPCK(hipStreamSynchronize(g.stream));
-      // every peer gets our n records; we get each peer's
-      std::vector<uint64_t> sendk, senda;
-      for(uint32_t p = 0; p < nr; ++p)
-      {
-        sb[p] = (p == rank() ? 0 : n) * sizeof(uint64_t);
-        rb[p] = (p == rank() ? 0 : cnt[p]) * sizeof(uint64_t);
-        if(p != rank()) { sendk.insert(sendk.end(), lk.begin(), lk.end()); senda.insert(senda.end(), la.begin(), la.end()); }
-      }
-      std::vector<uint64_t> rk(total), ra(total);
-      if(g.xp_a2a(g.xp_ctx, sendk.data(), sb.data(), rk.data(), rb.data()) != 0) return GPU_ACTOR_ECOMM;
-      if(g.xp_a2a(g.xp_ctx, senda.data(), sb.data(), ra.data(), rb.data()) != 0) return GPU_ACTOR_ECOMM;
-      uint64_t at = 0;
-      for(uint32_t p = 0; p < nr; ++p)
-      {
-        if(p == rank() || !cnt[p]) continue;
-        HIPCK(hipMemcpyAsync(g.d_skey[1] + off[p], rk.data() + at, cnt[p] * sizeof(uint64_t),
-          hipMemcpyHostToDevice, g.stream));
-        HIPCK(hipMemcpyAsync(g.d_sarg[1] + off[p], ra.data() + at, cnt[p] * sizeof(uint64_t),
-          hipMemcpyHostToDevice, g.stream));
-        at += cnt[p];
-      }
-      HIPCK(hipStreamSynchronize(g.stream));
-    }
-    else
-    {
-      NCCLCK(ncclGroupStart());
+      uint64_t* mine_d = part ? g.d_sarg[0] : g.d_skey[0];
+      uint64_t* all_d = part ? g.d_sarg[1] : g.d_skey[1];
+      std::vector<XcPeer> pp(nr);
       for(uint32_t p = 0; p < nr; ++p)
       {
         if(p == rank()) continue;
-        if(n)
-        {
-          NCCLCK(ncclSend(g.d_skey[0], n, ncclUint64, p, g.comm, g.stream));
-          NCCLCK(ncclSend(g.d_sarg[0], n, ncclUint64, p, g.comm, g.stream));
-        }
-        if(cnt[p])
-        {
-          NCCLCK(ncclRecv(g.d_skey[1] + off[p], cnt[p], ncclUint64, p, g.comm, g.stream));
-          NCCLCK(ncclRecv(g.d_sarg[1] + off[p], cnt[p], ncclUint64, p, g.comm, g.stream));
-        }
+        pp[p].d_send = mine_d;
+        pp[p].send = (uint64_t)n * sizeof(uint64_t);
+        pp[p].d_recv = all_d + off[p];
+        pp[p].recv = cnt[p] * sizeof(uint64_t);
       }
-      NCCLCK(ncclGroupEnd());
+      const int rc = xc_sendrecv(pp);
+      if(rc) return rc;
     }
     // sort input: the gathered list
     HIPCK(hipMemcpyAsync(g.d_skey[0], g.d_skey[1], total * sizeof(uint64_t),
@@ -1336,15 +1398,14 @@ int launch_pending(uint32_t slot)
 int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out)
 {
   out.resize(n);
-  if(R() > 1 && !g.xp_ar)
-    NCCLCK(ncclAllReduce(g.d_pend + first, g.d_pend + first, n, ncclUint64, ncclSum, g.comm,
-      g.stream));
+  if(R() > 1)
+  {
+    const int rc = xc_allreduce_sum(g.d_pend + first, g.d_pend + first, n, XC_U64);
+    if(rc) return rc;
+  }
   HIPCK(hipMemcpyAsync(out.data(), g.d_pend + first, n * sizeof(unsigned long long),
     hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
-  if(R() > 1 && g.xp_ar &&
-    g.xp_ar(g.xp_ctx, reinterpret_cast<uint64_t*>(out.data()), n) != 0)
-    return GPU_ACTOR_ECOMM;
   return 0;
 }
 
@@ -1413,8 +1474,8 @@ void free_all()
   if(g.d_xc) (void)hipFree(g.d_xc);
   if(g.h_xc) (void)hipHostFree(g.h_xc);
   if(g.d_spill_flag) (void)hipFree(g.d_spill_flag);
-  if(g.h_xout) (void)hipHostFree(g.h_xout);
-  if(g.h_xin) (void)hipHostFree(g.h_xin);
+  if(g.h_sbuf) (void)hipHostFree(g.h_sbuf);
+  if(g.h_rbuf) (void)hipHostFree(g.h_rbuf);
   for(hipEvent_t e : g.ev) (void)hipEventDestroy(e);
   if(g.comm) (void)ncclCommDestroy(g.comm);
   if(g.stream) (void)hipStreamDestroy(g.stream);
@@ -1530,8 +1591,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_stats, ST_COUNT * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats, 0, ST_COUNT * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
-  HIPCK(hipMalloc(&g.d_dbg, kMaxZones * 8 * sizeof(unsigned long long)));
-  HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * 8 * sizeof(unsigned long long), g.stream));
+  HIPCK(hipMalloc(&g.d_dbg, kMaxZones * kDbgSlots * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * kDbgSlots * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_spawn_n, sizeof(unsigned int)));
   HIPCK(hipMemsetAsync(g.d_spawn_n, 0, sizeof(unsigned int), g.stream));
   HIPCK(hipMalloc(&g.d_tstart, GPU_ACTOR_MAX_TYPES * sizeof(uint32_t)));
@@ -1561,8 +1622,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_trig_n, 4 * sizeof(unsigned int)));
   HIPCK(hipMemsetAsync(g.d_trig_n, 0, 4 * sizeof(unsigned int), g.stream));
   HIPCK(hipMalloc(&g.d_bigc, kBigCopyCap * sizeof(BigCopy)));
-  HIPCK(hipMalloc(&g.d_bigc_n, 2 * sizeof(unsigned int)));
-  HIPCK(hipMemsetAsync(g.d_bigc_n, 0, 2 * sizeof(unsigned int), g.stream));
+  HIPCK(hipMalloc(&g.d_bigc_n, 2 * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_bigc_n, 0, 2 * sizeof(unsigned long long), g.stream));
   HIPCK(hipHostMalloc(&g.h_ctl, sizeof(SparseCtl), hipHostMallocDefault));
   HIPCK(hipMemsetAsync(g.d_live, 0, GPU_ACTOR_MAX_TYPES * sizeof(unsigned long long), g.stream));
 
@@ -1579,10 +1640,9 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
     }
     else
     {
-      // host transport (callbacks registered with gpu_actor_set_transport)
+      // host transport (callbacks registered with gpu_actor_set_transport);
+      // its staging grows on demand (stage_room)
       if(!g.xp_a2a || !g.xp_ar) return GPU_ACTOR_EINVAL;
-      HIPCK(hipHostMalloc(&g.h_xout, (size_t)R() * g.xcap * sizeof(XRec), hipHostMallocDefault));
-      HIPCK(hipHostMalloc(&g.h_xin, (size_t)R() * g.xcap * sizeof(XRec), hipHostMallocDefault));
     }
     HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
     HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
@@ -1688,7 +1748,8 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.d_xc = nullptr; g.h_xc = nullptr; g.d_spill_flag = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
   g.xin_cap = 0; g.d_xspill = nullptr; g.d_xspill_n = nullptr; g.xspill_cap = 0;
-  g.h_xout = g.h_xin = nullptr;
+  g.h_sbuf = g.h_rbuf = nullptr;
+  g.h_sbuf_cap = g.h_rbuf_cap = 0;
   return 0;
 }
 
@@ -2265,35 +2326,13 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   int rc = launch_pending(kPendPre);
   if(rc) return rc;
   const unsigned long long* src_stats = g.d_stats;
-  if(R() > 1 && g.xp_ar)
-  {
-    // host transport: sum counters and pending over ranks on the host
-    std::vector<uint64_t> hv(ST_COUNT + 1);
-    HIPCK(hipMemcpyAsync(hv.data(), g.d_stats, ST_COUNT * sizeof(uint64_t),
-      hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipMemcpyAsync(hv.data() + ST_COUNT, g.d_pend + kPendPre, sizeof(uint64_t),
-      hipMemcpyDeviceToHost, g.stream));
-    HIPCK(hipStreamSynchronize(g.stream));
-    if(g.xp_ar(g.xp_ctx, hv.data(), hv.size()) != 0) return GPU_ACTOR_ECOMM;
-    memcpy(st, hv.data(), sizeof(st));
-    memset(out, 0, sizeof(*out));
-    out->steps = g.steps_total;
-    out->delivered = st[ST_DELIVERED];
-    out->sent = st[ST_SENT];
-    out->pending = hv[ST_COUNT];
-    out->dropped = st[ST_DROPPED] + st[ST_XCHG_OVERFLOW];
-    out->remote = g.remote_total;
-    out->active = st[ST_ACTIVE];
-    for(int t = 0; t < GPU_ACTOR_MAX_TYPES; ++t) out->delivered_by_type[t] = st[ST_BY_TYPE + t];
-    out->atomics = st[ST_ATOMICS];
-    return 0;
-  }
   if(R() > 1)
   {
     // sum counters and pending over ranks into scratch (pend[0 .. ST_COUNT))
-    NCCLCK(ncclAllReduce(g.d_stats, g.d_pend, ST_COUNT, ncclUint64, ncclSum, g.comm, g.stream));
-    NCCLCK(ncclAllReduce(g.d_pend + kPendPre, g.d_pend + kPendPre, 1, ncclUint64,
-      ncclSum, g.comm, g.stream));
+    rc = xc_allreduce_sum(g.d_stats, g.d_pend, ST_COUNT, XC_U64);
+    if(rc) return rc;
+    rc = xc_allreduce_sum(g.d_pend + kPendPre, g.d_pend + kPendPre, 1, XC_U64);
+    if(rc) return rc;
     src_stats = g.d_pend;
   }
   HIPCK(hipMemcpyAsync(st, src_stats, sizeof(st), hipMemcpyDeviceToHost, g.stream));
@@ -2338,12 +2377,12 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
 }
 
 // Diagnostic (not in the public header): phase stamps of the last k_step of
-// a -DGPA_STAMPS build, [n_zones][8] shader-clock values.
+// a -DGPA_STAMPS build, [n_zones][kDbgSlots] shader-clock values.
 GPU_ACTOR_API int gpu_actor_debug_stamps(uint64_t* out, uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init || !out) return GPU_ACTOR_ESTATE;
-  n = std::min<uint64_t>(n, (uint64_t)kMaxZones * 8);
+  n = std::min<uint64_t>(n, (uint64_t)kMaxZones * kDbgSlots);
   HIPCK(hipMemcpyAsync(out, g.d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   return 0;

@@ -43,6 +43,7 @@ constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above ever
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
 constexpr uint32_t kSeqApply = 0xFFFFu;          // outbox marker: reducible apply
 constexpr uint32_t kFanLds = 256;                // analyzers a zone accumulates in LDS
+constexpr uint32_t kDbgSlots = 16;               // diagnostic build: clock stamps per zone
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
@@ -120,12 +121,13 @@ struct TypeDev {
 
 // One deferred carry copy: records rec(from + j), j < rem, of an actor's
 // canonical mail (rec(k) = k < ncc ? c[k] : p[k - ncc]: its carried mail,
-// then its sorted arrivals) to dst[j].
+// then its sorted arrivals) to dst[j]. base: the copy's first record in the
+// step's list of all listed records (copies in slot order have rising bases).
 struct BigCopy {
   const ZRec* c;
   const ZRec* p;
   ZRec* dst;
-  uint32_t ncc, from, rem, pad;
+  uint32_t ncc, from, rem, base;
 };
 static_assert(sizeof(BigCopy) == 40, "BigCopy is 40 B");
 
@@ -189,7 +191,7 @@ struct EngDev {
   // workgroup; k_carry_big, launched right behind k_step, copies every listed
   // remainder across all CUs and clears the list.
   BigCopy* bigc;
-  unsigned int* bigc_n;           // [2]: listed copies, finished k_carry_big workgroups
+  unsigned long long* bigc_n;     // [2]: listed copies << 32 | their records, finished k_carry_big workgroups
   uint32_t bigc_cap, defer_big;
   // order-free zones run their behaviours twice instead of through the outbox
   // (zone_dev.h two_pass; PONYC_AMD_TWO_PASS=0 turns it off for A/B runs)

@@ -28,11 +28,14 @@
 namespace gpa {
 
 // Diagnostic build only (-DGPA_STAMPS): thread 0 of each zone stamps the
-// shader clock at phase boundaries into c_eng.dbg[zone * 8 + k]. The shipped
+// shader clock at phase boundaries into c_eng.dbg[zone * kDbgSlots + k]. The shipped
 // build compiles these away.
 #ifdef GPA_STAMPS
 #define GPA_STAMP(k)                                                         \
-  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
+  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * kDbgSlots + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
+// diagnostic build: add the clocks since t0 to slot k (thread 0)
+#define GPA_ACC(k, t0)                                                        \
+  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * kDbgSlots + (k)] += __builtin_amdgcn_s_memtime() - (t0); } while(0)
 #else
 #define GPA_STAMP(k) do {} while(0)
 #endif
@@ -833,10 +836,15 @@ template <int HT> __host__ __device__ constexpr bool two_pass()
 {
   return HT == GPU_ACTOR_HT_PINGER;     // order-free, at most one send per message
 }
+// state words a two-pass table keeps per actor (1 for the others: unused)
+template <int HT> __host__ __device__ constexpr int plan_words()
+{
+  if constexpr(HT >= 0 && two_pass<HT>()) return HT_Words<HT>::W; else return 1;
+}
 constexpr uint32_t kRounds = kZone / kZoneThreads;
 static_assert(kRounds == 4, "two rounds per packed count word, two words");
-// tile records after the per-actor counts at the head of the LDS pool
-constexpr uint32_t kPlanTile = kTile - kZone * sizeof(uint32_t) / sizeof(uint4);
+// pass 2's tile: the whole LDS pool (the per-actor counts are in registers by then)
+constexpr uint32_t kPlanTile = kTile;
 
 // Store record r = {to, w | src_local, arg lo, arg hi} at position pos of
 // bucket b's chunk: a destination zone's landing buffer (past its capacity:
@@ -918,6 +926,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_nout;
   __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
   __shared__ uint32_t s_tot;                // messages pending in the zone (fast path)
+  __shared__ uint32_t s_ph[64];             // two-pass path: actors per message count
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
@@ -950,6 +959,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     return;
   }
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
+  if(tid < 64) s_ph[tid] = 0;
   if constexpr(kFan)
     for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
   const uint32_t nxt = cur ^ 1u;
@@ -1048,6 +1058,32 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // arrivals comes back from the counting atomic and stays in a register
   // (packed rank << 11 | actor), so placing it needs no second pass over the
   // landing buffer. kIdxPer loads in flight per thread.
+  // The zone's type when one type covers all of its slots, else -1. It is
+  // wave-uniform, so that type's fields (batch, state, params) come through
+  // scalar loads instead of a per-lane lookup chain.
+  int tz = -1;
+  for(uint32_t t = 0; t < c_eng.n_types; ++t)
+    if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
+      tz = (int)t;
+  tz = __builtin_amdgcn_readfirstlane(tz);
+  // A zone of a two-pass table that may take that path (no backpressure
+  // anywhere, one type) loads its actors' state now, coalesced, so that the
+  // loads land while the landing buffer is counted; dropped if it does not.
+  constexpr int kPW = plan_words<HTS>();
+  uint64_t st[kRounds][kPW];
+  if constexpr(HTS >= 0 && two_pass<HTS>())
+    if(!gate && ztc == 0 && tz >= 0)
+    {
+      const TypeDev& T = c_types[tz];
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        const uint32_t i = r * kZoneThreads + tid;
+#pragma unroll
+        for(int k = 0; k < kPW; ++k)
+          st[r][k] = i < nact ? T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] : 0ull;
+      }
+    }
   uint32_t wr[kIdxPer];
   if(use_idx)
   {
@@ -1089,14 +1125,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.land_n[cur][z] = 0;
   }
 
-  // The zone's type when one type covers all of its slots, else -1. It is
-  // wave-uniform, so that type's fields (batch, state, params) come through
-  // scalar loads instead of a per-lane lookup chain.
-  int tz = -1;
-  for(uint32_t t = 0; t < c_eng.n_types; ++t)
-    if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
-      tz = (int)t;
-  tz = __builtin_amdgcn_readfirstlane(tz);
 
   // An order-free table (its behaviours ignore the message: the message-ubench
   // pinger) needs only each actor's message count when nothing can be left
@@ -1106,17 +1134,29 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // then never read — no segment scan, no index, no group sort. Otherwise
   // the zone takes the general path below.
   bool fast = false, plan = false;
+  // two-pass tables: each round's own actor's message count, and its rank
+  // among the zone's actors of the same count class (the plan path deals the
+  // actors to threads by count)
+  uint32_t own_n[kRounds], pk[kRounds], prk[kRounds];
   if constexpr(HTS >= 0 && order_free<HTS>())
     if(!gate && ztc == 0 && tz >= 0)
     {
       const uint32_t bt = c_types[tz].prio ? 0xFFFFFFFFu : c_types[tz].batch;
       int over = 0;
       uint32_t tot = 0;
-      for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
       {
+        const uint32_t i = r * kZoneThreads + tid;
         const uint32_t c = s_cnt[i] + s_ccnt[i];
         over |= c > bt;
         tot += c;
+        if constexpr(two_pass<HTS>())
+        {
+          own_n[r] = i < nact ? c : 0u;
+          pk[r] = 63u - min(own_n[r], 63u);
+          prk[r] = agg_add(s_ph, pk[r], true);
+        }
       }
       tot = (uint32_t)min(wave_sum((unsigned long long)tot), 0xFFFFFFFFull);
       if(lane == 0 && tot) atomicAdd(&s_tot, tot);
@@ -1272,27 +1312,68 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       uint32_t* const s_bs = s_dyn + nb;        // [nb] next free position of each chunk
       uint32_t* const s_cur = s_dyn + 2 * nb;   // [nb] the round's tile cursors
       uint32_t* const s_rh = s_dyn + 3 * nb;    // [2][nb] sends per (round, bucket), 16-bit halves
-      uint4* const tile = s_pool + kZone * sizeof(uint32_t) / sizeof(uint4);
+      uint4* const tile = s_pool;                // pass 2 (the whole pool)
       for(uint32_t b = tid; b < 2 * nb; b += kZoneThreads) s_rh[b] = 0;
-      // every round's actor state, loaded at once (one memory round per thread)
-      uint64_t st[kRounds][NW];
-      uint32_t nm[kRounds];
+      // Lanes of a wave run their actors' behaviours side by side, so a wave
+      // takes as long as its busiest lane, and the four waves a SIMD holds
+      // share its VALU. The zone's actors are therefore dealt to threads by
+      // message count: counting-sorted (busiest first; the class histogram
+      // s_ph was filled beside the fast check) into 64-actor blocks, and
+      // block (wave w, round r) = 8g + (r or 7 - r) for j = w (or W - 1 - w
+      // on odd rounds), g = j / 2 — every wave gets alike counts in its lanes
+      // and a like total over its rounds, and every round a like share of
+      // the zone's sends (the tile). The state moves through LDS (coalesced
+      // loads — issued before the count phase — and stores; the permuted
+      // threads read and write it there).
+      constexpr bool kStageApart =
+        kZone * sizeof(uint32_t) + NW * kZone * sizeof(uint64_t) + kZone * sizeof(uint16_t)
+          <= kTile * sizeof(uint4);
+      uint64_t* const s_stage = reinterpret_cast<uint64_t*>(s_pool) + (kStageApart ? kZone / 2 : 0);
+      uint16_t* const s_perm = reinterpret_cast<uint16_t*>(s_pool + kTile) - kZone;
+      static_assert(NW * kZone * sizeof(uint64_t) + kZone * sizeof(uint16_t) <= kTile * sizeof(uint4),
+                    "two-pass state stage and permutation fit the pool");
+      if(wv == 0)
+      {
+        const uint32_t c = s_ph[lane];
+        s_ph[lane] = wave_incl_scan(c, lane) - c;
+      }
+      lds_sync();
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+        s_perm[s_ph[pk[r]] + prk[r]] = (uint16_t)(r * kZoneThreads + tid);
+      lds_sync();
+      uint32_t ai[kRounds], nm[kRounds];
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
       {
-        const uint32_t i = r * kZoneThreads + tid;
-        nm[r] = i < nact ? s_cnt[i] : 0u;
+        const uint32_t j = (r & 1u) ? (uint32_t)kZoneWaves - 1u - wv : wv;
+        const uint32_t blk = 8u * (j >> 1) + ((j & 1u) ? 7u - r : r);
+        ai[r] = s_perm[64u * blk + lane];
+        nm[r] = s_cnt[ai[r]];
+      }
+      if constexpr(!kStageApart)
+        lds_sync();                            // every s_cnt read done: the stage overwrites it
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
 #pragma unroll
         for(int k = 0; k < NW; ++k)
-          st[r][k] = nm[r] ? T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] : 0ull;
-      }
+          s_stage[k * kZone + r * kZoneThreads + tid] = st[r][k];
       lds_sync();
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+#pragma unroll
+        for(int k = 0; k < NW; ++k)
+          st[r][k] = s_stage[k * kZone + ai[r]];
+#ifdef GPA_STAMPS
+      GPA_STAMP(8);                           // the permuted state is in registers
+      if(tid == 0) { c_eng.dbg[blockIdx.x * kDbgSlots + 9] = 0; c_eng.dbg[blockIdx.x * kDbgSlots + 10] = 0; }
+#endif
       // pass 1: count the sends of each round per bucket
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
       {
         if(!nm[r]) continue;
-        const uint32_t i = r * kZoneThreads + tid;
+        const uint32_t i = ai[r];
         PlanCtx pc;
         pc.reset_common();
         pc.li = L0 + i - T.lfirst;
@@ -1307,6 +1388,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         for(uint32_t j = 0; j < nm[r]; ++j) handle(HtTag<HTS>{}, T, pc, sc, 0u, 0ull);
       }
       lds_sync();
+      GPA_STAMP(3);
       // one chunk per bucket for the zone's sends
       for(uint32_t b = tid; b < nb; b += kZoneThreads)
       {
@@ -1330,9 +1412,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       tc.tile = tile; tc.cur = s_cur; tc.st = s_st; tc.bs = s_bs;
       tc.L0 = L0; tc.nz = nz; tc.nxt = nxt; tc.xover = 0;
       uint32_t dz = 0;
+#ifdef GPA_STAMPS
+      unsigned long long emit_clk = 0, t_emit = 0;    // diagnostic build: Σ tile-emit time
+#endif
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
       {
+#ifdef GPA_STAMPS
+        const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
+#endif
         // the round's bucket starts in the tile: an exclusive scan of its
         // counts, each thread a contiguous run of buckets
         {
@@ -1362,9 +1450,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         }
         const uint32_t tr = s_tmp[kZoneWaves - 1];     // the round's sends
         lds_sync();
+#ifdef GPA_STAMPS
+        GPA_ACC(9, t_scan);
+        const unsigned long long t_hand = __builtin_amdgcn_s_memtime();
+#endif
         if(nm[r])
         {
-          const uint32_t i = r * kZoneThreads + tid;
+          const uint32_t i = ai[r];
           const uint32_t L = L0 + i;
           tc.li = L - T.lfirst;
           tc.self = L * R + me;
@@ -1372,8 +1464,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           tc.type = tz;
           tc.seq = 0;
           for(uint32_t j = 0; j < nm[r]; ++j) handle(HtTag<HTS>{}, T, tc, st[r], 0u, 0ull);
-#pragma unroll
-          for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + tc.li] = st[r][k];
           // overloaded iff a full batch ran (batch_limit_reached, actor.c:369-381);
           // nothing here mutes
           const bool full = T.prio ? (nm[r] % T.batch == 0u) : nm[r] == T.batch;
@@ -1384,6 +1474,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           dz += nm[r];
         }
         lds_sync();
+#ifdef GPA_STAMPS
+        GPA_ACC(10, t_hand);
+        t_emit = __builtin_amdgcn_s_memtime();
+#endif
         // the tile, sorted by bucket, to the chunks: runs of one chunk per wave store
         const uint32_t m = min(tr, kPlanTile);
         for(uint32_t q = tid; q < m; q += kZoneThreads)
@@ -1393,10 +1487,33 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           xover += emit_rec(rec, b, s_bs[b] + (q - s_st[b]), L0, nz, nxt);
         }
         lds_sync();
+#ifdef GPA_STAMPS
+        emit_clk += __builtin_amdgcn_s_memtime() - t_emit;
+#endif
         // the chunks' next free positions
         for(uint32_t b = tid; b < nb; b += kZoneThreads)
           s_bs[b] += (s_rh[(r >> 1) * nb + b] >> ((r & 1u) * 16u)) & 0xFFFFu;
       }
+      // the new state back through the stage: permuted into LDS, coalesced out
+      // (the last round's emit is behind a barrier: the pool is free)
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+#pragma unroll
+        for(int k = 0; k < NW; ++k)
+          s_stage[k * kZone + ai[r]] = st[r][k];
+      lds_sync();
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        const uint32_t i = r * kZoneThreads + tid;
+        if(own_n[r])
+#pragma unroll
+          for(int k = 0; k < NW; ++k)
+            T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] = s_stage[k * kZone + i];
+      }
+#ifdef GPA_STAMPS
+      if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 2] = emit_clk;
+#endif
       sent = tc.sent;
       xover += tc.xover;
       if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
@@ -1555,13 +1672,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         // until then); a full list: copied here
         if(tid == 0)
         {
-          const uint32_t slot = atomicAdd(&c_eng.bigc_n[0], 1u);
+          // one atomic gives the slot and the copy's place in the flat list
+          const unsigned long long v = atomicAdd(&c_eng.bigc_n[0], (1ull << 32) | rem);
+          const uint32_t slot = (uint32_t)(v >> 32);
           uint32_t ok = 0;
           if(slot < c_eng.bigc_cap)
           {
             BigCopy b;
             b.c = C + s_cst[i]; b.p = Sz + s_off[i]; b.dst = cout + co;
-            b.ncc = s_ccnt[i]; b.from = n - rem; b.rem = rem; b.pad = 0;
+            b.ncc = s_ccnt[i]; b.from = n - rem; b.rem = rem; b.base = (uint32_t)v;
             c_eng.bigc[slot] = b;
             ok = 1;
           }

@@ -24,9 +24,9 @@ lib.gpu_actor_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nz = (100_004 + 2047) // 2048
 for step in range(4):
     e.run_fixed(1)
-    buf = np.zeros(nz * 8, dtype=np.uint64)
+    buf = np.zeros(nz * 16, dtype=np.uint64)
     lib.gpu_actor_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-    st = buf.reshape(nz, 8).astype(np.int64)[0]
+    st = buf.reshape(nz, 16).astype(np.int64)[0]
     order = [(0, 1, "count"), (1, 2, "scans"), (2, 3, "place"), (3, 7, "big sort"),
              (7, 4, "behaviours+carry"), (4, 5, "reserve"), (5, 6, "scatter")]
     parts = {nm: int(st[b] - st[a]) for a, b, nm in order}
