@@ -1,7 +1,8 @@
 # Round evidence for the shipped build: -m gpu suite, smoke, the full bench
 # (with the CPU baseline), rocprofv3 kernel stats of the bench, and the k_step
 # PMC traffic passes (one rocprofv3 run per pass). Each GPU step has its own
-# limit; the first failure ends the call.
+# limit; the first failure ends the call. SKIP_FULL_BENCH=1 leaves out the
+# full bench (CPU baselines, ring); the hot-receiver burst/backlog steps close it.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -14,8 +15,10 @@ echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 tail -3 gpurun_out/smoke_$TAG.log
-timeout -k 10 600 python bench.py > gpurun_out/bench_full_$TAG.json 2> gpurun_out/bench_full_$TAG.err || exit $?
-cat gpurun_out/bench_full_$TAG.json
+if [ -z "$SKIP_FULL_BENCH" ]; then
+  timeout -k 10 600 python bench.py > gpurun_out/bench_full_$TAG.json 2> gpurun_out/bench_full_$TAG.err || exit $?
+  cat gpurun_out/bench_full_$TAG.json
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/$TAG -o run -- \
   python3 bench.py --no-cpu-baseline --no-ring > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err || exit $?
 find gpurun_out/prof/$TAG -name '*kernel_stats*'
@@ -48,3 +51,7 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/general_$TAG -o run -- \
   python3 scripts/profile_general.py > gpurun_out/general_prof_$TAG.jsonl 2> gpurun_out/general_prof_$TAG.err || exit $?
 cat gpurun_out/general_prof_$TAG.jsonl
+for r in 1 2; do
+  timeout -k 10 180 python scripts/hot_receiver_bench.py > gpurun_out/hot_${TAG}_$r.jsonl 2>&1 || exit $?
+  cat gpurun_out/hot_${TAG}_$r.jsonl
+done
