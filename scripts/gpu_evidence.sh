@@ -55,3 +55,8 @@ for r in 1 2; do
   timeout -k 10 180 python scripts/hot_receiver_bench.py > gpurun_out/hot_${TAG}_$r.jsonl 2>&1 || exit $?
   cat gpurun_out/hot_${TAG}_$r.jsonl
 done
+# every BASELINE config beside the reference runtime (CONFIGS=1)
+if [ -n "$CONFIGS" ]; then
+  timeout -k 10 600 python scripts/bench_configs.py --cpu > gpurun_out/configs_$TAG.jsonl 2> gpurun_out/configs_$TAG.err || exit $?
+  cat gpurun_out/configs_$TAG.jsonl
+fi
