@@ -39,18 +39,6 @@ StepEntry step_entry_storm();
 StepEntry step_entry_spreader();
 } // namespace gpa_z12
 
-// the 1024-actor-zone instantiations (step_*_z10.hip; no pinger: its
-// order-free two-pass path needs four drain rounds per zone)
-namespace gpa_z10 {
-StepEntry step_entry_any();
-StepEntry step_entry_ring();
-StepEntry step_entry_pinger_det();
-StepEntry step_entry_fanin_sender();
-StepEntry step_entry_gups_streamer();
-StepEntry step_entry_storm();
-StepEntry step_entry_spreader();
-} // namespace gpa_z10
-
 using namespace gpa;
 
 // gups Updater tables (gups_basic/main.pony:145-155: table[k] = k + index*size),
@@ -455,10 +443,7 @@ const std::vector<StepEntry>& step_entries()
     gpa_z12::step_entry_any(), gpa_z12::step_entry_ring(), gpa_z12::step_entry_pinger(),
     gpa_z12::step_entry_pinger_det(), gpa_z12::step_entry_fanin_sender(),
     gpa_z12::step_entry_gups_streamer(), gpa_z12::step_entry_storm(),
-    gpa_z12::step_entry_spreader(),
-    gpa_z10::step_entry_any(), gpa_z10::step_entry_ring(), gpa_z10::step_entry_pinger_det(),
-    gpa_z10::step_entry_fanin_sender(), gpa_z10::step_entry_gups_streamer(),
-    gpa_z10::step_entry_storm(), gpa_z10::step_entry_spreader()};
+    gpa_z12::step_entry_spreader()};
   return v;
 }
 
@@ -473,26 +458,6 @@ bool defer_big_wanted()
     if(t.created && !reducible_ht(t.ht) && t.ht != GPU_ACTOR_HT_PINGER && t.ht != GPU_ACTOR_HT_RING)
       return true;
   return false;
-}
-
-// Dynamic LDS of a staged k_step unit: all the workgroup may hold, less the
-// unit's static LDS (queried once per kernel).
-uint32_t staged_dyn_lds(const StepEntry& se)
-{
-  static std::vector<std::pair<step_kernel_t, uint32_t>> cache;
-  for(const auto& c : cache)
-    if(c.first == se.kernel) return c.second;
-  int dev = 0, max_lds = 0;
-  hipFuncAttributes fa;
-  if(hipGetDevice(&dev) != hipSuccess ||
-     hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
-     hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(se.kernel)) != hipSuccess)
-    return 0;
-  const uint32_t dyn = (uint32_t)std::max<int64_t>(0, ((int64_t)max_lds - (int64_t)fa.sharedSizeBytes) & ~15ll);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(se.kernel),
-    hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  cache.emplace_back(se.kernel, dyn);
-  return dyn;
 }
 
 int upload_types()
@@ -554,20 +519,11 @@ int upload_types()
     const char* f = getenv("PONYC_AMD_TWO_PASS");
     e.two_pass = (f && atoi(f) == 0) ? 0u : 1u;
   }
-  {
-    const char* f = getenv("PONYC_AMD_STAGE");
-    e.stage = (f && atoi(f) == 0) ? 0u : 1u;
-  }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
-  // every k_step code object holds its own copy of the constants (a staged
-  // unit with the dynamic LDS it is launched with)
+  // every k_step code object holds its own copy of the constants
   for(const StepEntry& se : step_entries())
-  {
-    EngDev eu = e;
-    if(se.staged) eu.dyn_lds = staged_dyn_lds(se);
-    HIPCK(se.upload(td, &eu, g.stream));
-  }
+    HIPCK(se.upload(td, &e, g.stream));
   return 0;
 }
 
@@ -699,10 +655,7 @@ uint32_t pick_zone_bits(uint64_t n)
   const uint64_t rb = R() > 1 ? R() : 0;
   const uint64_t nz11 = (n + 2047) / 2048, nz12 = (n + 4095) / 4096;
   if(const char* f = getenv("PONYC_AMD_ZONE_BITS"))      // test hook: force a geometry
-  {
-    const int b = atoi(f);
-    return b == 12 ? 12u : (b == 10 && (n + 1023) / 1024 + rb <= kMaxZones) ? 10u : 11u;
-  }
+    return atoi(f) == 12 ? 12u : 11u;
   return (nz11 + rb > 640 && nz12 + rb <= 2300) ? 12u : 11u;
 }
 
@@ -1254,17 +1207,6 @@ StepEntry pick_step_entry()
   }
   if(mixed) only = -1;
   const bool z12 = g.zbits == 12;
-  if(g.zbits == 10)
-    switch(only)
-    {
-      case GPU_ACTOR_HT_RING: return gpa_z10::step_entry_ring();
-      case GPU_ACTOR_HT_PINGER_DET: return gpa_z10::step_entry_pinger_det();
-      case GPU_ACTOR_HT_FANIN_SENDER: return gpa_z10::step_entry_fanin_sender();
-      case GPU_ACTOR_HT_GUPS_STREAMER: return gpa_z10::step_entry_gups_streamer();
-      case GPU_ACTOR_HT_STORM: return gpa_z10::step_entry_storm();
-      case GPU_ACTOR_HT_SPREADER: return gpa_z10::step_entry_spreader();
-      default: return gpa_z10::step_entry_any();
-    }
   switch(only)
   {
     case GPU_ACTOR_HT_RING: return z12 ? gpa_z12::step_entry_ring() : gpa::step_entry_ring();
@@ -1396,16 +1338,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
   // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
   // (five for an order-free zone's two passes: zone_dev.h two_pass)
-  const size_t nb = g.n_zones + (R() > 1 ? R() : 0);
-  size_t dyn = sizeof(uint32_t) * std::max<size_t>(5 * nb, se.sort_work);
-  if(se.staged)
-  {
-    // all the LDS: the pool, then (phase 4) three bucket arrays or (phase 3)
-    // the hot-group sort's work area, the histogram at the end
-    dyn = staged_dyn_lds(se);
-    if(se.pool_bytes + sizeof(uint32_t) * (std::max<size_t>(3 * nb, se.sort_work) + nb) > dyn)
-      return GPU_ACTOR_ENOMEM;
-  }
+  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(5 * (g.n_zones + (R() > 1 ? R() : 0)),
+                                                          se.sort_work);
   step_kernel_t kern = se.kernel;
   if(e0)
   {

@@ -24,19 +24,7 @@ namespace gpa {
 
 constexpr int      kBlock = 256;                 // helper kernels
 constexpr int      kWaves = kBlock / 64;
-// Zone geometry (A/B builds override it: scripts/build_variants.sh). A k_step
-// unit of a table that reads its messages (GPA_STAGED_TU: every table but the
-// order-free pinger) runs 1024-thread workgroups with all of the CU's LDS and
-// stages each slice of its zone's mail there before the behaviours run
-// (zone_dev.h, staged drain); -DGPA_NO_STAGE builds the unstaged form.
-#if defined(GPA_STAGED_TU) && !defined(GPA_NO_STAGE)
-#define GPA_STAGE 1
-#ifndef GPA_ZONE_THREADS
-#define GPA_ZONE_THREADS 1024
-#endif
-#else
-#define GPA_STAGE 0
-#endif
+// Zone geometry (A/B builds override it: scripts/build_variants.sh)
 #ifndef GPA_ZONE_BITS
 #define GPA_ZONE_BITS 11
 #endif
@@ -207,12 +195,7 @@ struct EngDev {
   uint32_t bigc_cap, defer_big;
   // order-free zones run their behaviours twice instead of through the outbox
   // (zone_dev.h two_pass; PONYC_AMD_TWO_PASS=0 turns it off for A/B runs)
-  uint32_t two_pass;
-  // staged k_step units (GPA_STAGE): bytes of dynamic LDS the host launches
-  // them with (set per unit at upload), and whether the drain stages mail in
-  // it (PONYC_AMD_STAGE=0 turns it off for A/B runs)
-  uint32_t dyn_lds;
-  uint32_t stage, pad7;
+  uint32_t two_pass, pad7;
 };
 
 

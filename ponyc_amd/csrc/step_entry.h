@@ -25,8 +25,6 @@ struct StepEntry {
   uint32_t zone_bits;      // actors per zone = 1 << zone_bits
   uint32_t threads;        // workgroup size
   uint32_t sort_work;      // u32 of dynamic LDS the hot-group sort borrows
-  bool staged;             // takes all of the CU's LDS as dynamic memory (GPA_STAGE)
-  uint32_t pool_bytes;     // staged: the LDS pool at the start of that memory (zone_dev.h)
 };
 
 namespace gpa {

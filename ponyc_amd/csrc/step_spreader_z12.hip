@@ -1,5 +1,4 @@
 // k_step<GPU_ACTOR_HT_SPREADER> at 4096-actor zones, 1024-thread workgroups (step_entry.h).
-#define GPA_STAGED_TU 1   // mail staged in LDS before the behaviours run (engine_dev.h)
 #define GPA_ZONE_BITS 12
 #define GPA_ZONE_THREADS 1024
 #define GPA_IDX_CAP 24576

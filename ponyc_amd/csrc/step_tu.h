@@ -32,12 +32,10 @@ hipError_t step_upload(const void* types, const void* eng, hipStream_t s)
 
 #if GPA_STEP_STUB
 StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork, GPA_STAGE != 0,
-                                      (uint32_t)(kTile * sizeof(uint4)) }; }
+                                      (uint32_t)kZoneThreads, kSortWork }; }
 #else
 StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload, false, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork, GPA_STAGE != 0,
-                                      (uint32_t)(kTile * sizeof(uint4)) }; }
+                                      (uint32_t)kZoneThreads, kSortWork }; }
 #endif
 
 } // namespace gpa

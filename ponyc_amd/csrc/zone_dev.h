@@ -312,43 +312,6 @@ struct AccS {
   }
 };
 
-// AccStage: the actor's segment staged in LDS (staged drain: a slice of the
-// zone's mail loaded there by the whole workgroup before the behaviours run).
-// Its LDS index entries are permuted alongside, so the index stays the
-// actor's canonical order for the carry-out, which reads through it.
-struct AccStage {
-  uint4* st;          // the segment's records: st[0, n)
-  uint16_t* idx;      // the segment's index entries
-  __device__ __forceinline__ ZRec rec(uint32_t j) const
-  {
-    const uint4 v = st[j];
-    ZRec r;
-    r.w0 = v.x; r.from = v.y; r.arg = ((uint64_t)v.w << 32) | v.z;
-    return r;
-  }
-  // insertion sort of [lo, lo + g) by canonical key
-  __device__ void sort(uint32_t lo, uint32_t g)
-  {
-    for(uint32_t i = 1; i < g; ++i)
-    {
-      const uint4 x = st[lo + i];
-      const uint16_t xi = idx[lo + i];
-      const uint64_t kx = ((uint64_t)x.y << 16) | (x.x >> 16);
-      uint32_t j = i;
-      while(j > 0)
-      {
-        const uint4 y = st[lo + j - 1];
-        if((((uint64_t)y.y << 16) | (y.x >> 16)) <= kx) break;
-        st[lo + j] = y;
-        idx[lo + j] = idx[lo + j - 1];
-        --j;
-      }
-      st[lo + j] = x;
-      idx[lo + j] = xi;
-    }
-  }
-};
-
 // Groups handled whole up to this size keep their keys in registers.
 constexpr uint32_t kMedReg = 16;
 
@@ -869,19 +832,17 @@ __device__ __forceinline__ uint32_t zone_actor(const TypeDev& T, ZoneCtx& a, Acc
 // counts give each bucket's start), and the tile leaves as runs of one chunk
 // each. The behaviours are deterministic functions of the state, so both
 // passes make the same sends. A drain round is one actor per thread.
-constexpr uint32_t kRounds = kZone / kZoneThreads;
 template <int HT> __host__ __device__ constexpr bool two_pass()
 {
-  // order-free, at most one send per message; the packed per-round counts
-  // below assume four drain rounds
-  return HT == GPU_ACTOR_HT_PINGER && kRounds == 4;
+  return HT == GPU_ACTOR_HT_PINGER;     // order-free, at most one send per message
 }
 // state words a two-pass table keeps per actor (1 for the others: unused)
 template <int HT> __host__ __device__ constexpr int plan_words()
 {
   if constexpr(HT >= 0 && two_pass<HT>()) return HT_Words<HT>::W; else return 1;
 }
-static_assert(kRounds == 4 || !two_pass<GPU_ACTOR_HT_PINGER>(), "two rounds per packed count word, two words");
+constexpr uint32_t kRounds = kZone / kZoneThreads;
+static_assert(kRounds == 4, "two rounds per packed count word, two words");
 // pass 2's tile: the whole LDS pool (the per-actor counts are in registers by then)
 constexpr uint32_t kPlanTile = kTile;
 
@@ -948,18 +909,9 @@ template <int HTS>
 __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
   uint32_t sidx)
 {
-  // The pool. Phases 1-3: per-actor arrays + the segment index; phase 4: the
-  // outbox sort tile (kTile records). Staged units take all LDS as dynamic
-  // memory: [pool | (phase 4) bucket bases, tile counts and starts, or (phase
-  // 3) the hot-group sort's work area | ... | bucket histogram], and during the
-  // drain the stage fills the gap between the index's used part and the
-  // histogram (see the staged drain below).
-#if GPA_STAGE
-  extern __shared__ uint4 s_lds[];
-  uint4* const s_pool = s_lds;
-#else
+  // 64 KB pool. Phases 1-3: per-actor arrays + the segment index; phase 4:
+  // the outbox sort tile (kTile records).
   __shared__ uint4 s_pool[kTile];
-#endif
   static_assert(4 * kZone * sizeof(uint32_t) + kIdxCap * sizeof(uint16_t) <= sizeof(uint4) * kTile,
                 "LDS pool too small");
   uint32_t* const s_cnt = reinterpret_cast<uint32_t*>(s_pool);   // records per actor this step
@@ -968,9 +920,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   uint32_t* const s_aux = s_ccnt + kZone;   // carry start -> landing cursor -> carry-out offset
   uint16_t* const s_idx = reinterpret_cast<uint16_t*>(s_aux + kZone);  // index into carry ++ landing
   uint32_t* const s_cst = reinterpret_cast<uint32_t*>(s_idx);   // S path: carry start per actor
-#if !GPA_STAGE
   extern __shared__ uint32_t s_dyn[];   // [nb] histogram, [nb] chunk bases, [nb] tile counts, [nb] tile starts
-#endif
   __shared__ uint32_t s_tmp[kZoneWaves + 1];
   __shared__ uint32_t s_tmp2[2 * kZoneWaves];
   __shared__ uint32_t s_nout;
@@ -1019,16 +969,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t nz = c_eng.n_zones;
   const uint32_t nb = nz + (R > 1 ? R : 0u);
   const uint32_t cap = zone_capacity(z);
-#if GPA_STAGE
-  uint32_t* const s_hist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_lds) + c_eng.dyn_lds) - nb;
-  uint32_t* const s_xtra = reinterpret_cast<uint32_t*>(s_pool + kTile);
-  uint32_t* const s_dyn = s_xtra;           // (the two-pass path's arrays: not in staged units)
-#else
-  uint32_t* const s_hist = s_dyn;
-  uint32_t* const s_xtra = s_dyn + nb;
-#endif
-  uint32_t* const s_base = s_xtra;           // [nb] chunk bases (phase 4)
-  uint32_t* const s_work = GPA_STAGE ? s_xtra : s_dyn;   // the hot-group sort's work area (phase 3)
+  uint32_t* s_hist = s_dyn;
+  uint32_t* s_base = s_dyn + nb;
 
   // Backpressure bookkeeping: ztc = this zone's actors that
   // trigger muting after the last step (overloaded or muted); ztn = nonzero
@@ -1337,16 +1279,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         bool ok;
         if(use_idx)
           ok = coop_sort_group(AccIdx{s_idx + s_off[i], C, Ld, nc}, s_idx + s_off[i], nullptr,
-                               s_ccnt[i], g, ia, ia + g, nullptr, s_work, s_red3);
+                               s_ccnt[i], g, ia, ia + g, nullptr, s_dyn, s_red3);
         else
           ok = coop_sort_group(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, nullptr, Sz + s_off[i],
                                s_ccnt[i], g, ia,
-                               ia + g, Sz + 2 * cap, s_work, s_red3);
+                               ia + g, Sz + 2 * cap, s_dyn, s_red3);
         if(ok && tid == 0) s_bigbits[i >> 5] |= 1u << (i & 31);
       }
-      // (unstaged units: the work area overlapped the histogram)
-      if(!GPA_STAGE)
-        for(uint32_t b = tid; b < max(nb, kSortWork); b += kZoneThreads) s_dyn[b] = 0;
+      for(uint32_t b = tid; b < max(nb, kSortWork); b += kZoneThreads) s_dyn[b] = 0;
       __syncthreads();
     }
   }
@@ -1600,10 +1540,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
   // drain local actor i, of type t (T = c_types[t])
   uint8_t* const trig_cur = gate ? c_eng.trig[cur] : nullptr;
-  // stg: the slice of mail staged in LDS that holds this actor's segment, from
-  // segment position p0 (staged drain), or null
-  auto drain_actor = [&](const TypeDev& T, int t, uint32_t i, uint4* stg, uint32_t p0)
-    __attribute__((always_inline)) {
+  auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
     const uint32_t n = s_cnt[i];
     const uint32_t L = L0 + i;
     a.li = L - T.lfirst;
@@ -1621,19 +1558,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     a.yield_req = 0;
     const bool stays = (tb & 2u) && (c_eng.trig[cur][c_eng.muted_on[L]] & 1u);
     uint32_t d = 0;
-#if GPA_STAGE
-#define ZDRAIN_STAGED(HT)                                                             \
-    if(stg)                                                                           \
-    {                                                                                 \
-      AccStage acc{stg + (s_off[i] - p0), s_idx + s_off[i]};                          \
-      d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
-    }                                                                                 \
-    else
-#else
-#define ZDRAIN_STAGED(HT)
-#endif
 #define ZDRAIN(HT)                                                                    \
-    ZDRAIN_STAGED(HT)                                                                 \
     if(use_idx)                                                                       \
     {                                                                                 \
       AccIdx acc{s_idx + s_off[i], C, Ld, nc};                                        \
@@ -1667,7 +1592,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
     }
 #undef ZDRAIN
-#undef ZDRAIN_STAGED
     // overloaded iff a full batch ran (a priority type's last batch) and the
     // actor was not muted (batch_limit_reached, actor.c:369-381; maybe_mute
     // first, 449-460)
@@ -1684,87 +1608,26 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     active += d ? 1u : 0u;
     return d;
   };
-  // one actor with mail or trigger bytes (reducible types have neither)
-  uint32_t dz = 0;
-  auto drain_one = [&](uint32_t i, uint4* stg, uint32_t p0) __attribute__((always_inline)) {
-    if(s_cnt[i] == 0 && s_tb[i] == 0) return;
-    if(tz >= 0)
-    {
-      dz += drain_actor(c_types[tz], tz, i, stg, p0);
-      return;
-    }
-    const int t = type_of_local(L0 + i);
-    if(t < 0 || c_types[t].reducible) return;
-    const uint32_t d = drain_actor(c_types[t], t, i, stg, p0);
-    if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
-  };
-  if(tz < 0 || !c_types[tz].reducible)
+  if(tz >= 0)
   {
-    // Staged drain (staged units, LDS-index zones): the zone's actors run in
-    // slices — consecutive actors, at most one per thread, whose segments
-    // fit the stage — and each slice's mail is first loaded into LDS by the
-    // whole workgroup, all loads in flight at once, in segment order. The
-    // behaviours then read their messages from LDS instead of one dependent
-    // gather per actor from the landing buffer (whose lines hold records of
-    // eight random actors). The stage is the LDS between the index's used
-    // part and the histogram; an actor whose segment alone exceeds it drains
-    // from HBM in a slice of its own.
-    bool staged = false;
-    uint4* stage = nullptr;
-    uint32_t scap = 0;
-    if constexpr(GPA_STAGE)
-      if(use_idx && c_eng.stage != 0u)
-      {
-        const uint32_t ntot = nc + nl;
-        const uint32_t st0 = kZone + (2u * ntot + 15u) / 16u;          // in 16-B units
-        const uint32_t st1 = (c_eng.dyn_lds - 4u * nb) / 16u;
-        stage = s_pool + st0;
-        scap = st1 > st0 ? st1 - st0 : 0u;
-        staged = scap >= (uint32_t)kZoneThreads;
-      }
-    if(staged)
-    {
-      for(uint32_t a0 = 0; a0 < nact; )
-      {
-        const uint32_t p0 = s_off[a0];
-        const uint32_t ia = a0 + tid;
-        // segment ends rise with the actor: the actors that fit are a prefix
-        const bool fits = ia < nact && s_off[ia] + s_cnt[ia] - p0 <= scap;
-        const uint32_t nf = (uint32_t)__syncthreads_count(fits);   // (the last slice's reads are done)
-        const uint32_t a1 = a0 + (nf ? nf : 1u);
-        if(nf)
-        {
-          const uint32_t p1 = s_off[a1 - 1] + s_cnt[a1 - 1];
-          for(uint32_t j0 = p0; j0 < p1; j0 += kZoneThreads * kUnroll)
-          {
-            uint4 r[kUnroll];
-#pragma unroll
-            for(int u = 0; u < kUnroll; ++u)
-            {
-              const uint32_t j = j0 + u * kZoneThreads + tid;
-              if(j < p1)
-              {
-                const uint32_t x = s_idx[j];
-                r[u] = *reinterpret_cast<const uint4*>(x < nc ? C + x : Ld + (x - nc));
-              }
-            }
-#pragma unroll
-            for(int u = 0; u < kUnroll; ++u)
-            {
-              const uint32_t j = j0 + u * kZoneThreads + tid;
-              if(j < p1) stage[j - p0] = r[u];
-            }
-          }
-          lds_sync();
-        }
-        if(ia < a1) drain_one(ia, nf ? stage : nullptr, p0);
-        a0 = a1;
-      }
-    }
-    else
-      for(uint32_t i = tid; i < nact; i += kZoneThreads) drain_one(i, nullptr, 0u);
+    const TypeDev& T = c_types[tz];
+    uint32_t dz = 0;
+    if(!T.reducible)
+      for(uint32_t i = tid; i < nact; i += kZoneThreads)
+        if(s_cnt[i] || s_tb[i]) dz += drain_actor(T, tz, i);
+    if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
   }
-  if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
+  else
+  {
+    for(uint32_t i = tid; i < nact; i += kZoneThreads)
+    {
+      if(s_cnt[i] == 0 && s_tb[i] == 0) continue;
+      const int t = type_of_local(L0 + i);
+      if(t < 0 || c_types[t].reducible) continue;
+      const uint32_t d = drain_actor(c_types[t], t, i);
+      if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
+    }
+  }
   sent = a.sent;
   applied = a.applied;
   if(applied && a.applied_type >= 0)
@@ -1910,8 +1773,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // ---- 4. one chunk per destination bucket ----------------------------------------
   if(!plan)
   {
-  uint32_t* s_tcnt = s_xtra + nb;       // records of the tile per bucket
-  uint32_t* s_tst = s_xtra + 2 * nb;    // bucket start within the sorted tile
+  uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
+  uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
   for(uint32_t b = tid; b < nb; b += kZoneThreads)
   {
     const uint32_t h = s_hist[b];

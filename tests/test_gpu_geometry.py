@@ -1,12 +1,9 @@
-"""GPU parity with the other zone geometries: 4096-actor zones
-(1024-thread workgroups, step_*_z12.hip) and 1024-actor zones (one drain
-round per workgroup, step_*_z10.hip), and the staged units with their LDS
-stage turned off (PONYC_AMD_STAGE=0: every actor drains from HBM).
+"""GPU parity with 4096-actor zones (1024-thread workgroups, step_*_z12.hip).
 
-The engine picks 4096-actor zones by itself only for large engines (over ~640
+The engine picks that geometry by itself only for large engines (over ~640
 buckets of 2048-actor zones: C5's 8M actors in test_gpu_fullsize.py); the
-PONYC_AMD_ZONE_BITS hook (engine.hip: pick_zone_bits) forces a geometry here
-so that small, oracle-checked workloads run every path of each one —
+PONYC_AMD_ZONE_BITS hook (engine.hip: pick_zone_bits) forces it here so that
+small, oracle-checked workloads run every path of the second geometry —
 landing, carry and backpressure, hot groups, the small-step path, spawning
 and two ranks' exchange."""
 import numpy as np
@@ -18,16 +15,9 @@ from test_gpu_parity import _both, _assert_same
 pytestmark = pytest.mark.gpu
 
 
-GEOMETRIES = {"z12": {"PONYC_AMD_ZONE_BITS": "12"},
-              "z10": {"PONYC_AMD_ZONE_BITS": "10"},
-              "z11_unstaged": {"PONYC_AMD_STAGE": "0"}}
-
-
-@pytest.fixture(params=list(GEOMETRIES))
-def geometry(request, monkeypatch):
-    for k, v in GEOMETRIES[request.param].items():
-        monkeypatch.setenv(k, v)
-    return request.param
+@pytest.fixture(autouse=True)
+def zone_bits_12(monkeypatch):
+    monkeypatch.setenv("PONYC_AMD_ZONE_BITS", "12")
 
 
 CASES = {
@@ -51,7 +41,7 @@ CASES = {
 
 
 @pytest.mark.parametrize("name", list(CASES))
-def test_parity_geometry(engine_factory, oracle, geometry, name):
+def test_parity_zones_4096(engine_factory, oracle, name):
     setup, result = CASES[name]
     g, o = _both(engine_factory, oracle, setup, result)
     _assert_same(g, o)

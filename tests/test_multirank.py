@@ -58,11 +58,10 @@ def test_two_ranks_one_gpu(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bits", ["12", "10"])
 @pytest.mark.parametrize("case", ["ubench_det", "storm", "spreader", "mute", "spill_one_rank",
                                   "xspill", "backlog"])
-def test_two_ranks_other_geometry(case, bits, monkeypatch):
-    """The same two-rank parity cases with 4096- or 1024-actor zones forced
-    (engine.hip: pick_zone_bits)."""
-    monkeypatch.setenv("PONYC_AMD_ZONE_BITS", bits)
+def test_two_ranks_zones_4096(case, monkeypatch):
+    """The same two-rank parity cases with 4096-actor zones forced
+    (engine.hip: pick_zone_bits), as large engines run them."""
+    monkeypatch.setenv("PONYC_AMD_ZONE_BITS", "12")
     test_two_ranks_one_gpu(case)
