@@ -233,8 +233,9 @@ __global__ void __launch_bounds__(kBlock) k_carry_big()
       for(uint32_t j = j0 + threadIdx.x; j < j1; j += kBlock)
       {
         const uint32_t k = b.from + j;
+        const uint32_t q = k - b.ncc;
         const uint4 r = k < b.ncc ? *reinterpret_cast<const uint4*>(b.c + k)
-                                  : *reinterpret_cast<const uint4*>(b.p + (k - b.ncc));
+                      : *reinterpret_cast<const uint4*>(b.p + (b.perm ? (uint32_t)(b.perm[q] & 0xFFFFFull) : q));
         *reinterpret_cast<uint4*>(b.dst + j) = r;
       }
     }
@@ -447,16 +448,23 @@ const std::vector<StepEntry>& step_entries()
   return v;
 }
 
-// Backlog copies go to k_carry_big when some serial type can leave mail over
-// in order (every table but the order-free pinger and the ring, whose token
-// never queues); elsewhere the extra launch per step would buy nothing.
-// PONYC_AMD_DEFER_BIG=0/1 forces it (tests, A/B).
+// Backlog copies go to k_carry_big (the whole GPU copies them right after
+// k_step) in engines whose serial actors run more than one handler table —
+// the fan-in shapes (sources and sinks of different kinds) that build
+// backlogs of thousands of records per actor. The extra launch per step costs
+// 2.4 % of a C2-det step and 1 % of a C5 step (profiles/r04j_hot_msd.txt,
+// PONYC_AMD_DEFER_BIG=0/1), where backlogs over 128 records are rare and a
+// zone copies one itself. PONYC_AMD_DEFER_BIG=0/1 forces it (tests, A/B).
 bool defer_big_wanted()
 {
   if(const char* f = getenv("PONYC_AMD_DEFER_BIG")) return atoi(f) != 0;
+  int only = -1;
   for(const HostType& t : g.types)
-    if(t.created && !reducible_ht(t.ht) && t.ht != GPU_ACTOR_HT_PINGER && t.ht != GPU_ACTOR_HT_RING)
-      return true;
+  {
+    if(!t.created || reducible_ht(t.ht)) continue;
+    if(only >= 0 && (uint32_t)only != t.ht) return true;
+    only = (int)t.ht;
+  }
   return false;
 }
 

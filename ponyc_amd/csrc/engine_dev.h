@@ -121,15 +121,18 @@ struct TypeDev {
 
 // One deferred carry copy: records rec(from + j), j < rem, of an actor's
 // canonical mail (rec(k) = k < ncc ? c[k] : p[k - ncc]: its carried mail,
-// then its sorted arrivals) to dst[j]. base: the copy's first record in the
-// step's list of all listed records (copies in slot order have rising bases).
+// then its sorted arrivals — read through perm, the sorted items
+// key << 20 | position, when the workgroup sorted them) to dst[j]. base: the
+// copy's first record in the step's list of all listed records (copies in
+// slot order have rising bases).
 struct BigCopy {
   const ZRec* c;
   const ZRec* p;
   ZRec* dst;
+  const uint64_t* perm;
   uint32_t ncc, from, rem, base;
 };
-static_assert(sizeof(BigCopy) == 40, "BigCopy is 40 B");
+static_assert(sizeof(BigCopy) == 48, "BigCopy is 48 B");
 
 struct EngDev {
   uint32_t n_types, rank, nranks, n_local;

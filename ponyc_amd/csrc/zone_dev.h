@@ -223,6 +223,25 @@ __device__ __forceinline__ uint32_t agg_add(uint32_t* ctr, uint32_t key, bool va
   return res;
 }
 
+// agg_add without the ranks: counting only (the leader's add returns nothing,
+// so no lane waits for an LDS round trip).
+template <int kMinRun = 0>
+__device__ __forceinline__ void agg_count(uint32_t* ctr, uint32_t key, bool valid)
+{
+  const uint32_t lane = __lane_id();
+  uint64_t active = __ballot(valid);
+  for(int it = 0; it < 4 && active; ++it)
+  {
+    const int leader = __ffsll((long long)active) - 1;
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const uint64_t peers = __ballot(valid && key == k) & active;
+    if(kMinRun > 0 && __popcll(peers) < kMinRun) break;
+    if((int)lane == leader) atomicAdd(&ctr[k], (uint32_t)__popcll(peers));
+    active &= ~peers;
+  }
+  if((active >> lane) & 1ull) atomicAdd(&ctr[key], 1u);
+}
+
 // 16-B record moves built from their four words. Written this way, the
 // scatter tile's records stay in registers and go to LDS as one ds_write_b128
 // each; the plain uint4 copy made the compiler split the LDS stores and spill
@@ -287,9 +306,13 @@ struct AccS {
   ZRec* p;            // arrivals: p[0, g)
   const ZRec* c;      // carried mail: c[0, nc)
   uint32_t nc;
+  // a group the workgroup sorted: its sorted items (key << kPayBits | position
+  // in p), read through instead of permuting the records themselves
+  const uint64_t* perm = nullptr;
   __device__ __forceinline__ ZRec rec(uint32_t j) const
   {
-    return j < nc ? ld_rec(c + j) : ld_rec(p + (j - nc));
+    if(j < nc) return ld_rec(c + j);
+    return ld_rec(p + (perm ? (uint32_t)(perm[j - nc] & 0xFFFFFull) : j - nc));
   }
   // insertion sort of the arrival group [lo, lo + g), lo == nc
   __device__ void sort(uint32_t lo, uint32_t g)
@@ -551,6 +574,7 @@ __device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, ui
 constexpr uint32_t kBigGroup = 128;
 constexpr uint32_t kMaxBig = 32;            // big groups sorted per round of the loop
 constexpr uint32_t kPayBits = 20;           // payload bits of an item (group <= 2^20)
+static_assert(kPayBits == 20, "AccS::perm masks positions with 0xFFFFF");
 constexpr uint32_t kSortWork = 512 + kZoneWaves * 256;   // u32 of LDS the sort borrows
 
 // Stable sort of n items in a by item bits [lo, hi); b is scratch of n items.
@@ -683,14 +707,146 @@ __device__ __forceinline__ uint32_t bits_for(uint32_t v)
   return v ? 32u - (uint32_t)__clz(v) : 0u;
 }
 
+// Items of a hot group have distinct keys (a sender's sequence numbers are),
+// so the group need not be sorted stably: one MSD pass partitions the items by
+// the top kMsdBits bits of their key into bins (a histogram, one scan, one
+// scatter with LDS cursors), and each bin — about a dozen items at the group
+// sizes that take this path — is then sorted whole by one thread in registers.
+// Three passes over the items instead of the LSD sort's key-width / 8 passes
+// of ranking and scattering each. Bins larger than kMsdReg items are sorted
+// in memory; a group whose largest bin exceeds kMsdMaxBin (keys that cluster)
+// takes the LSD sort.
+constexpr uint32_t kMsdBits = 11;           // bins of the MSD pass (2048 u32 of the sort's LDS)
+constexpr uint32_t kMsdReg = 16;            // items a thread sorts in registers
+constexpr uint32_t kMsdMaxBin = 64;
+static_assert((1u << kMsdBits) + kZoneWaves + 1 <= kSortWork, "MSD bins fit the sort's LDS");
+
+// Sort n items in a by item bits [lo, lo + kbits) (keys distinct within
+// them); b is scratch of n items. The result ends in a. All threads call;
+// ends behind a barrier.
+__device__ void coop_msd_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t kbits,
+  uint32_t* s_work)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t d = min(kMsdBits, kbits);
+  const uint32_t sh = lo + kbits - d;
+  const uint32_t nb = 1u << d;
+  uint32_t* s_bin = s_work;                     // [nb] counts -> starts -> cursors (ends)
+  uint32_t* s_tmp = s_work + (1u << kMsdBits);  // [kZoneWaves + 1]
+  for(uint32_t k = tid; k < nb; k += kZoneThreads) s_bin[k] = 0;
+  lds_sync();
+  for(uint32_t i0 = 0; i0 < n; i0 += kZoneThreads * kUnroll)
+  {
+    uint64_t x[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t i = i0 + u * kZoneThreads + tid;
+      x[u] = i < n ? a[i] : 0ull;
+    }
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      if(i0 + u * kZoneThreads + tid < n) atomicAdd(&s_bin[(uint32_t)(x[u] >> sh) & (nb - 1u)], 1u);
+  }
+  lds_sync();
+  // the largest bin decides the path (uniform)
+  uint32_t mx = 0;
+  for(uint32_t k = tid; k < nb; k += kZoneThreads) mx = max(mx, s_bin[k]);
+#pragma unroll
+  for(int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+  if(lane == 0) s_tmp[wv] = mx;
+  lds_sync();
+  mx = 0;
+  for(uint32_t w = 0; w < (uint32_t)kZoneWaves; ++w) mx = max(mx, s_tmp[w]);
+  lds_sync();
+  if(mx > kMsdMaxBin)
+  {
+    coop_radix_sort(a, b, n, lo, lo + ((kbits + 7u) & ~7u), s_work);
+    return;
+  }
+  (void)block_scan_n(s_bin, s_bin, nb, s_tmp);     // counts -> bin starts (in place)
+  {
+    // half-batches, software-pipelined (loads of one half before the other's stores)
+    constexpr int kH = kUnroll / 2;
+    constexpr uint32_t kStride = kZoneThreads * kH;
+    auto load_half = [&](uint64_t (&x)[kH], uint32_t i0) __attribute__((always_inline)) {
+#pragma unroll
+      for(int u = 0; u < kH; ++u)
+      {
+        const uint32_t i = i0 + u * kZoneThreads + tid;
+        x[u] = i < n ? a[i] : 0ull;
+      }
+    };
+    auto scatter_half = [&](const uint64_t (&x)[kH], uint32_t i0) __attribute__((always_inline)) {
+#pragma unroll
+      for(int u = 0; u < kH; ++u)
+        if(i0 + u * kZoneThreads + tid < n)
+          b[atomicAdd(&s_bin[(uint32_t)(x[u] >> sh) & (nb - 1u)], 1u)] = x[u];
+    };
+    uint64_t xa[kH], xb[kH];
+    load_half(xa, 0);
+    for(uint32_t i0 = 0; i0 < n; i0 += 2 * kStride)
+    {
+      load_half(xb, i0 + kStride);
+      scatter_half(xa, i0);
+      load_half(xa, i0 + 2 * kStride);
+      scatter_half(xb, i0 + kStride);
+    }
+  }
+  // the scatter's stores are the bin sorts' loads (other threads); s_bin[k]
+  // is now the end of bin k
+  __syncthreads();
+  for(uint32_t k = tid; k < nb; k += kZoneThreads)
+  {
+    const uint32_t e = s_bin[k], s0 = k ? s_bin[k - 1] : 0u, m = e - s0;
+    if(m <= 1)
+    {
+      if(m) a[s0] = b[s0];
+      continue;
+    }
+    if(m <= kMsdReg)
+    {
+      uint64_t r[kMsdReg];
+#pragma unroll
+      for(int j = 0; j < (int)kMsdReg; ++j) r[j] = (uint32_t)j < m ? b[s0 + j] : ~0ull;
+      // insertion network over static indices (stays in registers)
+#pragma unroll
+      for(int i = 1; i < (int)kMsdReg; ++i)
+#pragma unroll
+        for(int j = i; j > 0; --j)
+        {
+          const uint64_t p = r[j - 1], q = r[j];
+          r[j - 1] = p < q ? p : q;
+          r[j] = p < q ? q : p;
+        }
+#pragma unroll
+      for(int j = 0; j < (int)kMsdReg; ++j)
+        if((uint32_t)j < m) a[s0 + j] = r[j];
+    }
+    else
+    {
+      // a larger bin: insertion sort in memory, into a
+      for(uint32_t i = 0; i < m; ++i)
+      {
+        const uint64_t x = b[s0 + i];
+        uint32_t j = i;
+        while(j > 0 && a[s0 + j - 1] > x) { a[s0 + j] = a[s0 + j - 1]; --j; }
+        a[s0 + j] = x;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Sort the arrival group [nc, nc + g) of one actor's segment, by the whole
-// workgroup. idx path: payload = the idx entry; S path: payload = position,
-// and the arrivals (seg[0, g)) are permuted through scratch `tmp` (g
-// records). Returns false (nothing changed) when the compressed key does not
-// fit.
+// workgroup. idx path: payload = the idx entry, written back in order; S
+// path: payload = the record's position in the segment, and the sorted items
+// are left in ia (g of them) for the actor's accessor to read through
+// (AccS::perm) — the records themselves do not move. ib is scratch of g
+// items. Returns false (nothing changed) when the compressed key does not fit.
 template <class Acc>
-__device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, uint32_t g,
-  uint64_t* ia, uint64_t* ib, ZRec* tmp, uint32_t* s_work, uint32_t* s_red3)
+__device__ bool coop_sort_group(Acc acc, uint16_t* idx, uint32_t nc, uint32_t g,
+  uint64_t* ia, uint64_t* ib, uint32_t* s_work, uint32_t* s_red3)
 {
   const uint32_t tid = threadIdx.x;
   // key range: min/max sender, max sequence
@@ -722,26 +878,41 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
   const uint32_t sbits = bits_for(smax), kbits = bits_for(fmax - fmin) + sbits;
   const uint32_t pay = idx ? 16u : kPayBits;
   if(kbits + pay > 64u) return false;
-  for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
   {
-    ZRec r[kUnroll];
+    // half-batches, software-pipelined: one half's record loads are issued
+    // before the other half's item stores (vmcnt counts both, in order)
+    constexpr int kH = kUnroll / 2;
+    constexpr uint32_t kStride = kZoneThreads * kH;
+    auto load_half = [&](ZRec (&r)[kH], uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-    {
-      const uint32_t j = j0 + u * kZoneThreads + tid;
-      if(j < g) r[u] = acc.rec(nc + j);
-    }
+      for(int u = 0; u < kH; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j < g) r[u] = acc.rec(nc + j);
+      }
+    };
+    auto store_half = [&](const ZRec (&r)[kH], uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
+      for(int u = 0; u < kH; ++u)
+      {
+        const uint32_t j = j0 + u * kZoneThreads + tid;
+        if(j >= g) continue;
+        const uint64_t key = ((uint64_t)(r[u].from - fmin) << sbits) | (r[u].w0 >> 16);
+        ia[j] = (key << pay) | (idx ? (uint64_t)idx[nc + j] : (uint64_t)j);
+      }
+    };
+    ZRec ra[kH], rb[kH];
+    load_half(ra, 0);
+    for(uint32_t j0 = 0; j0 < g; j0 += 2 * kStride)
     {
-      const uint32_t j = j0 + u * kZoneThreads + tid;
-      if(j >= g) continue;
-      const uint64_t key = ((uint64_t)(r[u].from - fmin) << sbits) | (r[u].w0 >> 16);
-      ia[j] = (key << pay) | (idx ? (uint64_t)idx[nc + j] : (uint64_t)j);
+      load_half(rb, j0 + kStride);
+      store_half(ra, j0);
+      load_half(ra, j0 + 2 * kStride);
+      store_half(rb, j0 + kStride);
     }
   }
   __syncthreads();
-  coop_radix_sort(ia, ib, g, pay, pay + ((kbits + 7u) & ~7u), s_work);
+  coop_msd_sort(ia, ib, g, pay, kbits, s_work);
   const uint64_t pm = (1ull << pay) - 1;
   if(idx)
   {
@@ -762,47 +933,8 @@ __device__ bool coop_sort_group(Acc acc, uint16_t* idx, ZRec* seg, uint32_t nc, 
       }
     }
   }
-  else
-  {
-    // kUnroll records in flight per thread in both passes
-    for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
-    {
-      uint32_t p[kUnroll];
-#pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
-      {
-        const uint32_t j = j0 + u * kZoneThreads + tid;
-        p[u] = j < g ? (uint32_t)(ia[j] & pm) : 0u;
-      }
-      uint4 r[kUnroll];
-#pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
-        if(j0 + u * kZoneThreads + tid < g) r[u] = *reinterpret_cast<const uint4*>(seg + p[u]);
-#pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
-      {
-        const uint32_t j = j0 + u * kZoneThreads + tid;
-        if(j < g) *reinterpret_cast<uint4*>(tmp + j) = r[u];
-      }
-    }
-    __syncthreads();
-    for(uint32_t j0 = 0; j0 < g; j0 += kZoneThreads * kUnroll)
-    {
-      uint4 r[kUnroll];
-#pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
-      {
-        const uint32_t j = j0 + u * kZoneThreads + tid;
-        if(j < g) r[u] = *reinterpret_cast<const uint4*>(tmp + j);
-      }
-#pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
-      {
-        const uint32_t j = j0 + u * kZoneThreads + tid;
-        if(j < g) *reinterpret_cast<uint4*>(seg + j) = r[u];
-      }
-    }
-  }
+  // (S path: the sorted items stay in ia, and the actor's records are read
+  // through them: AccS::perm)
   __syncthreads();
   return true;
 }
@@ -1052,7 +1184,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
 #pragma unroll
     for(int u = 0; u < kUnroll; ++u)
-      (void)agg_add(s_ccnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
+      agg_count(s_ccnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
   }
   // Landed records: with the LDS index, each record's rank among its actor's
   // arrivals comes back from the counting atomic and stays in a register
@@ -1114,7 +1246,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     // (a hot receiver's arrivals: lanes of one actor folded into one atomic)
 #pragma unroll
     for(int u = 0; u < kUnroll; ++u)
-      (void)agg_add<8>(s_cnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
+      agg_count<8>(s_cnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
   }
   __syncthreads();
   GPA_STAMP(1);
@@ -1169,6 +1301,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         plan = fast && s_tot < c_eng.seq_max && c_eng.two_pass != 0u;
     }
   ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
+  // S path: the sorted items of the groups the workgroup sorted, each at its
+  // segment offset (S's last third, 2 cap items; read by the drain, the
+  // carry-out and k_carry_big)
+  uint64_t* const perm_s = reinterpret_cast<uint64_t*>(Sz + 2 * cap);
   if(fast)
   {
     // the actor's total (carried + landed); no group was sorted
@@ -1226,27 +1362,45 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       s_aux[i] = 0;
     }
     __syncthreads();
-    for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
-    {
-      uint4 r[kUnroll];
-      uint32_t pos[kUnroll];
-      // unconditional (clamped) loads: all in flight, the records in registers
+    // Two half-batches of kUnroll / 2 records per thread, software-pipelined:
+    // one half's loads are issued before the other half's stores, so waiting
+    // for a load never waits out the stores before it (vmcnt counts both, in
+    // issue order) — a hot receiver's zone places ~10^5 records here.
+    constexpr int kH = kUnroll / 2;
+    constexpr uint32_t kStride = kZoneThreads * kH;
+    auto load_half = [&](uint4 (&r)[kH], uint32_t b0) __attribute__((always_inline)) {
 #pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
+      for(int u = 0; u < kH; ++u)
       {
-        const uint32_t i = base + u * kZoneThreads + tid;
+        const uint32_t i = b0 + u * kZoneThreads + tid;
+        // unconditional (clamped) loads: all in flight, the records in registers
         r[u] = *reinterpret_cast<const uint4*>(Ld + min(i, nl - 1));
         if(i >= nl) r[u].x = 0xFFFFFFFFu;
       }
+    };
+    auto place_half = [&](const uint4 (&r)[kH]) __attribute__((always_inline)) {
+      uint32_t pos[kH];
 #pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
+      for(int u = 0; u < kH; ++u)
       {
         const uint32_t a = r[u].x & kZoneMask;
         pos[u] = s_off[a] + agg_add<8>(s_aux, a, r[u].x != 0xFFFFFFFFu);
       }
 #pragma unroll
-      for(int u = 0; u < kUnroll; ++u)
+      for(int u = 0; u < kH; ++u)
         if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
+    };
+    if(nl)
+    {
+      uint4 ra[kH], rb[kH];
+      load_half(ra, 0);
+      for(uint32_t b0 = 0; b0 < nl; b0 += 2 * kStride)
+      {
+        load_half(rb, b0 + kStride);
+        place_half(ra);
+        load_half(ra, b0 + 2 * kStride);
+        place_half(rb);
+      }
     }
   }
   // from here on s_cnt is the actor's total: carried + landed
@@ -1278,12 +1432,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         const uint32_t g = s_cnt[i] - s_ccnt[i];
         bool ok;
         if(use_idx)
-          ok = coop_sort_group(AccIdx{s_idx + s_off[i], C, Ld, nc}, s_idx + s_off[i], nullptr,
-                               s_ccnt[i], g, ia, ia + g, nullptr, s_dyn, s_red3);
+          ok = coop_sort_group(AccIdx{s_idx + s_off[i], C, Ld, nc}, s_idx + s_off[i],
+                               s_ccnt[i], g, ia, ia + g, s_dyn, s_red3);
         else
-          ok = coop_sort_group(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, nullptr, Sz + s_off[i],
-                               s_ccnt[i], g, ia,
-                               ia + g, Sz + 2 * cap, s_dyn, s_red3);
+          ok = coop_sort_group(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, nullptr,
+                               s_ccnt[i], g, perm_s + s_off[i], ia, s_dyn, s_red3);
         if(ok && tid == 0) s_bigbits[i >> 5] |= 1u << (i & 31);
       }
       for(uint32_t b = tid; b < max(nb, kSortWork); b += kZoneThreads) s_dyn[b] = 0;
@@ -1294,6 +1447,12 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(7);                          // diagnostic build: the hot-group sort ends
   auto big_sorted = [&](uint32_t i) __attribute__((always_inline)) {
     return ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
+  };
+  // S path accessor of actor i (a group the workgroup sorted: read through its items)
+  auto acc_s = [&](uint32_t i) __attribute__((always_inline)) {
+    AccS a_{Sz + s_off[i], C + s_cst[i], s_ccnt[i]};
+    if(big_sorted(i)) a_.perm = perm_s + s_off[i];
+    return a_;
   };
 
 
@@ -1566,7 +1725,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }                                                                                 \
     else                                                                              \
     {                                                                                 \
-      AccS acc{Sz + s_off[i], C + s_cst[i], s_ccnt[i]};                               \
+      AccS acc = acc_s(i);                                                            \
       d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
     }
     if constexpr(HTS >= 0)
@@ -1654,7 +1813,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       if(use_idx)
         carry_out(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
       else
-        carry_out(AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}, n - rem, n, z, co, nxt);
+        carry_out(acc_s(i), n - rem, n, z, co, nxt);
     }
     __syncthreads();
     const uint32_t nbig = min(s_nbig, kMaxBig);
@@ -1681,6 +1840,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
             BigCopy b;
             b.c = C + s_cst[i]; b.p = Sz + s_off[i]; b.dst = cout + co;
             b.ncc = s_ccnt[i]; b.from = n - rem; b.rem = rem; b.base = (uint32_t)v;
+            b.perm = big_sorted(i) ? perm_s + s_off[i] : nullptr;
             c_eng.bigc[slot] = b;
             ok = 1;
           }
@@ -1704,7 +1864,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           const uint32_t j = j0 + uu * kZoneThreads + tid;
           if(j < rem)
             r[uu] = use_idx ? AccIdx{s_idx + s_off[i], C, Ld, nc}.rec(n - rem + j)
-                            : AccS{Sz + s_off[i], C + s_cst[i], s_ccnt[i]}.rec(n - rem + j);
+                            : acc_s(i).rec(n - rem + j);
         }
       };
       auto store_half = [&](const ZRec (&r)[kH], uint32_t j0) __attribute__((always_inline)) {

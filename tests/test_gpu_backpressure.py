@@ -8,7 +8,7 @@ oracle (oracle/bsp.c restates the rules: DESIGN.md §2).
 - yield (ponyint_actor_yield, actor.c:675-679): the run ends after the
   behaviour; the rest of the mail waits, in order.
 - hot receivers: an arrival group above kBigGroup is sorted by the whole
-  workgroup (zone_dev.h coop_radix_sort), both with the LDS index (<= 16K
+  workgroup (zone_dev.h coop_msd_sort), both with the LDS index (<= 16K
   records in the zone) and with records materialised in S.
 Every case also checks that nothing was dropped."""
 import numpy as np
@@ -112,3 +112,16 @@ def test_backlog_copies(engine_factory, oracle, monkeypatch, defer, sources, sin
     _both(engine_factory, oracle,
           lambda e: W.fifo(e, sources, sinks, bursts, m, batch=batch, mailbox_cap=16),
           W.fifo_result, mailbox_cap=16)
+
+
+@pytest.mark.parametrize("m", [5, 20, 40])
+def test_hot_group_sort_paths(engine_factory, oracle, m):
+    """A hot sink's arrival group sorted by the workgroup (zone_dev.h
+    coop_msd_sort): 3000 sources burst m PUSHes each at one sink. The MSD
+    pass bins the keys by their top 11 bits — the sender id's high bits — so
+    each bin holds 2m items: m=5 sorts its bins in registers (15,000 arrivals:
+    the LDS-index path), m=20 in memory (over 16 items; the scratch path, read
+    through the sorted items), m=40 takes the LSD sort (bins over 64; the zone
+    also grows 4x in the burst)."""
+    _both(engine_factory, oracle, lambda e: W.fifo(e, 3000, 1, 1, m, mailbox_cap=16),
+          W.fifo_result)
