@@ -17,3 +17,7 @@ for r in 1 2; do
   timeout -k 10 240 python scripts/profile_general.py det storm pinger > gpurun_out/gen_${TAG}_$r.jsonl 2>&1 || exit $?
   cat gpurun_out/gen_${TAG}_$r.jsonl
 done
+if [ -n "$STAMPS" ]; then
+  timeout -k 10 180 python scripts/hot_stamps.py > gpurun_out/hot_stamps_$TAG.txt 2>&1 || exit $?
+  cat gpurun_out/hot_stamps_$TAG.txt
+fi
