@@ -724,7 +724,7 @@ static_assert((1u << kMsdBits) + kZoneWaves + 1 <= kSortWork, "MSD bins fit the 
 // Sort n items in a by item bits [lo, lo + kbits) (keys distinct within
 // them); b is scratch of n items. The result ends in a. All threads call;
 // ends behind a barrier.
-__device__ __attribute__((noinline)) void coop_msd_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t kbits,
+__device__ void coop_msd_sort(uint64_t* a, uint64_t* b, uint32_t n, uint32_t lo, uint32_t kbits,
   uint32_t* s_work)
 {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -845,7 +845,7 @@ __device__ __attribute__((noinline)) void coop_msd_sort(uint64_t* a, uint64_t* b
 // (AccS::perm) — the records themselves do not move. ib is scratch of g
 // items. Returns false (nothing changed) when the compressed key does not fit.
 template <class Acc>
-__device__ __attribute__((noinline)) bool coop_sort_group(Acc acc, uint16_t* idx, uint32_t nc, uint32_t g,
+__device__ bool coop_sort_group(Acc acc, uint16_t* idx, uint32_t nc, uint32_t g,
   uint64_t* ia, uint64_t* ib, uint32_t* s_work, uint32_t* s_red3)
 {
   const uint32_t tid = threadIdx.x;
@@ -1033,132 +1033,6 @@ struct TileCtx : ActorBase {
       xover += emit_rec(r, b, bs[b] + (idx - st[b]), L0, nz, nxt);
   }
 };
-
-// ---- scratch-path count and place (zones with more records than the LDS
-//      index holds: hot receivers) ---------------------------------------------------
-// Each lane keeps a small cache of (actor, count) pairs and adds a count to
-// LDS only when its actor leaves the cache: a hot receiver's zone (~10^5
-// arrivals over a handful of actors) then counts in registers, where one LDS
-// counter per actor taking every lane's add — or the ballots that fold them —
-// would serialise (burst count 0.39 -> 0.09 M clocks, profiles/r04o); elsewhere
-// every record misses and costs the one atomic it always did. A lane that
-// never evicted knows its exact count per actor and places those records in
-// blocks it reserves with one atomic each. The caches pass from count to place
-// through the index area of LDS (unused on this path past the carry starts).
-// Both are out of line: their registers stay out of k_step's drain.
-constexpr int kLc = (2 * 4 + 1) * kZoneThreads * 4 + kZone * 4 <= kIdxCap * 2 ? 4 : 3;
-static_assert((2 * kLc + 1) * kZoneThreads * 4 + kZone * 4 <= kIdxCap * 2, "lane caches fit the index area");
-
-__device__ __attribute__((noinline)) void sp_count_landed(const ZRec* Ld, uint32_t nl, uint32_t* s_cnt,
-  uint32_t* lc)
-{
-  const uint32_t tid = threadIdx.x;
-  uint32_t ck[kLc], cn[kLc];
-  uint32_t evict = 0;
-#pragma unroll
-  for(int c = 0; c < kLc; ++c) { ck[c] = 0xFFFFFFFFu; cn[c] = 0; }
-  for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
-  {
-    uint32_t w[kUnroll];
-#pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-    {
-      const uint32_t i = base + u * kZoneThreads + tid;
-      w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for(int u = 0; u < kUnroll; ++u)
-    {
-      if(w[u] == 0xFFFFFFFFu) continue;
-      const uint32_t a = w[u] & kZoneMask;
-      bool hit = false;
-#pragma unroll
-      for(int c = 0; c < kLc; ++c)
-        if(!hit && ck[c] == a) { cn[c]++; hit = true; }
-      if(!hit)
-      {
-        evict |= ck[kLc - 1] != 0xFFFFFFFFu ? 1u : 0u;
-        if(cn[kLc - 1]) atomicAdd(&s_cnt[ck[kLc - 1]], cn[kLc - 1]);
-#pragma unroll
-        for(int c = kLc - 1; c > 0; --c) { ck[c] = ck[c - 1]; cn[c] = cn[c - 1]; }
-        ck[0] = a; cn[0] = 1;
-      }
-    }
-  }
-#pragma unroll
-  for(int c = 0; c < kLc; ++c)
-  {
-    if(cn[c]) atomicAdd(&s_cnt[ck[c]], cn[c]);
-    lc[c * kZoneThreads + tid] = ck[c];
-    lc[(kLc + c) * kZoneThreads + tid] = cn[c];
-  }
-  lc[2 * kLc * kZoneThreads + tid] = evict;
-}
-
-// Records land in their actor's S segment (s_off: segment starts, s_aux:
-// cursors from 0). Two half-batches of kUnroll / 2 records per thread,
-// software-pipelined: one half's loads are issued before the other half's
-// stores, so waiting for a load never waits out the stores before it (vmcnt
-// counts both, in issue order).
-__device__ __attribute__((noinline)) void sp_place_landed(const ZRec* Ld, uint32_t nl,
-  const uint32_t* s_off, uint32_t* s_aux, ZRec* Sz, const uint32_t* lc)
-{
-  const uint32_t tid = threadIdx.x;
-  uint32_t ck[kLc], cb[kLc];
-  const bool blocks = lc[2 * kLc * kZoneThreads + tid] == 0u;
-#pragma unroll
-  for(int c = 0; c < kLc; ++c)
-  {
-    ck[c] = lc[c * kZoneThreads + tid];
-    const uint32_t n = lc[(kLc + c) * kZoneThreads + tid];
-    cb[c] = (blocks && n) ? atomicAdd(&s_aux[ck[c]], n) : 0u;
-  }
-  constexpr int kH = kUnroll / 2;
-  constexpr uint32_t kStride = kZoneThreads * kH;
-  auto load_half = [&](uint4 (&r)[kH], uint32_t b0) __attribute__((always_inline)) {
-#pragma unroll
-    for(int u = 0; u < kH; ++u)
-    {
-      const uint32_t i = b0 + u * kZoneThreads + tid;
-      // unconditional (clamped) loads: all in flight, the records in registers
-      r[u] = *reinterpret_cast<const uint4*>(Ld + min(i, nl - 1));
-      if(i >= nl) r[u].x = 0xFFFFFFFFu;
-    }
-  };
-  auto place_half = [&](const uint4 (&r)[kH]) __attribute__((always_inline)) {
-    uint32_t pos[kH];
-#pragma unroll
-    for(int u = 0; u < kH; ++u)
-    {
-      const uint32_t a = r[u].x & kZoneMask;
-      uint32_t rk = 0;
-      if(r[u].x == 0xFFFFFFFFu)
-        rk = 0;
-      else if(blocks)
-      {
-#pragma unroll
-        for(int c = 0; c < kLc; ++c)
-          if(ck[c] == a) rk = cb[c]++;
-      }
-      else
-        rk = atomicAdd(&s_aux[a], 1u);
-      pos[u] = s_off[a] + rk;
-    }
-#pragma unroll
-    for(int u = 0; u < kH; ++u)
-      if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
-  };
-  if(nl == 0) return;
-  uint4 ra[kH], rb[kH];
-  load_half(ra, 0);
-  for(uint32_t b0 = 0; b0 < nl; b0 += 2 * kStride)
-  {
-    load_half(rb, b0 + kStride);
-    place_half(ra);
-    load_half(ra, b0 + 2 * kStride);
-    place_half(rb);
-  }
-}
 
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
 // HTS >= 0: every serial actor of this engine runs handler table HTS (the host
@@ -1360,7 +1234,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
   }
   else
-    sp_count_landed(Ld, nl, s_cnt, reinterpret_cast<uint32_t*>(s_idx) + kZone);
+  for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
+  {
+    uint32_t w[kUnroll];
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+    {
+      const uint32_t i = base + u * kZoneThreads + tid;
+      w[u] = i < nl ? Ld[i].w0 : 0xFFFFFFFFu;
+    }
+    // (a hot receiver's arrivals: lanes of one actor folded into one atomic)
+#pragma unroll
+    for(int u = 0; u < kUnroll; ++u)
+      agg_count<8>(s_cnt, w[u] & kZoneMask, w[u] != 0xFFFFFFFFu);
+  }
   __syncthreads();
   GPA_STAMP(1);
   if(tid == 0)
@@ -1475,7 +1362,46 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       s_aux[i] = 0;
     }
     __syncthreads();
-    sp_place_landed(Ld, nl, s_off, s_aux, Sz, reinterpret_cast<const uint32_t*>(s_idx) + kZone);
+    // Two half-batches of kUnroll / 2 records per thread, software-pipelined:
+    // one half's loads are issued before the other half's stores, so waiting
+    // for a load never waits out the stores before it (vmcnt counts both, in
+    // issue order) — a hot receiver's zone places ~10^5 records here.
+    constexpr int kH = kUnroll / 2;
+    constexpr uint32_t kStride = kZoneThreads * kH;
+    auto load_half = [&](uint4 (&r)[kH], uint32_t b0) __attribute__((always_inline)) {
+#pragma unroll
+      for(int u = 0; u < kH; ++u)
+      {
+        const uint32_t i = b0 + u * kZoneThreads + tid;
+        // unconditional (clamped) loads: all in flight, the records in registers
+        r[u] = *reinterpret_cast<const uint4*>(Ld + min(i, nl - 1));
+        if(i >= nl) r[u].x = 0xFFFFFFFFu;
+      }
+    };
+    auto place_half = [&](const uint4 (&r)[kH]) __attribute__((always_inline)) {
+      uint32_t pos[kH];
+#pragma unroll
+      for(int u = 0; u < kH; ++u)
+      {
+        const uint32_t a = r[u].x & kZoneMask;
+        pos[u] = s_off[a] + agg_add<8>(s_aux, a, r[u].x != 0xFFFFFFFFu);
+      }
+#pragma unroll
+      for(int u = 0; u < kH; ++u)
+        if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
+    };
+    if(nl)
+    {
+      uint4 ra[kH], rb[kH];
+      load_half(ra, 0);
+      for(uint32_t b0 = 0; b0 < nl; b0 += 2 * kStride)
+      {
+        load_half(rb, b0 + kStride);
+        place_half(ra);
+        load_half(ra, b0 + 2 * kStride);
+        place_half(rb);
+      }
+    }
   }
   // from here on s_cnt is the actor's total: carried + landed
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_cnt[i] += s_ccnt[i];
