@@ -312,6 +312,22 @@ def lib_sha16(path: str) -> str | None:
         return None
 
 
+BENCH_WORKLOAD = "c2_message_ubench"
+
+
+def pmc_workload(path: str, d: dict) -> str:
+    """The workload a PMC summary was collected on: its `workload` field, or
+    (older summaries) the tag's suffix — pmc_k_step_<tag>_det / _storm are the
+    general-path passes of scripts/gpu_evidence.sh, not this bench's."""
+    if d.get("workload"):
+        return d["workload"]
+    stem = os.path.basename(path)[: -len(".json")]
+    for suffix in ("_det", "_storm"):
+        if stem.endswith(suffix):
+            return suffix[1:]
+    return BENCH_WORKLOAD
+
+
 def pmc_traffic(sha: str | None) -> tuple[float | None, str | None]:
     if sha is None:
         return None, None
@@ -320,7 +336,8 @@ def pmc_traffic(sha: str | None) -> tuple[float | None, str | None]:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("lib_sha16") == sha and d.get("hbm_bytes_per_launch"):
+        if (d.get("lib_sha16") == sha and d.get("hbm_bytes_per_launch")
+                and pmc_workload(f, d) == BENCH_WORKLOAD):
             return d["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 

@@ -9,7 +9,8 @@ are counted by these counters, so this is an upper bound on HBM bytes.
 Writes profiles/pmc_k_step_<tag>.json, which bench.py reports as
 roofline.traffic.
 
-usage: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> <tag>
+usage: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> <tag> [workload]
+(workload: c2_message_ubench — bench.py's, the default — or det / storm)
 """
 import csv
 import glob
@@ -19,6 +20,7 @@ import sys
 from collections import defaultdict
 
 d, tag = sys.argv[1], sys.argv[2]
+workload = sys.argv[3] if len(sys.argv) > 3 else "c2_message_ubench"
 vals = defaultdict(list)
 for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
@@ -29,6 +31,7 @@ mean = {k: sum(v) / len(v) for k, v in vals.items()}
 fetch_kb, write_kb = mean.get("FETCH_SIZE"), mean.get("WRITE_SIZE")
 out = {
     "kernel": "k_step",
+    "workload": workload,
     "dispatches": {k: len(v) for k, v in vals.items()},
     "fetch_size_kb": fetch_kb,
     "write_size_kb": write_kb,
