@@ -1,5 +1,5 @@
 # Same-box A/B of two engine builds (A = the in-tree library, B = $LIB_B):
-# the hot-path tests against A, then det / storm / pinger step times and the
+# the hot-path tests against B, then det / storm / pinger step times and the
 # hot-receiver burst for both, alternating, twice. Each GPU step has its own
 # limit; the first failure ends the call.
 set -o pipefail
@@ -9,8 +9,9 @@ TAG=${TAG:-ab2}
 A=$PWD/ponyc_amd/libgpuactor.so
 B=$PWD/$LIB_B
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
-  -k "fifo or backlog or mute or hot or fanin" > gpurun_out/pytest_$TAG.log 2>&1
+# the tests run against B (the candidate; the C-ABI program links the in-tree name)
+PONYC_AMD_LIB=$B timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
+  -k "(fifo or backlog or mute or hot or fanin) and not c_binary" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
