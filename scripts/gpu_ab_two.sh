@@ -11,7 +11,7 @@ B=$PWD/$LIB_B
 mkdir -p gpurun_out
 # the tests run against B (the candidate; the C-ABI program links the in-tree name)
 PONYC_AMD_LIB=$B timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
-  -k "(fifo or backlog or mute or hot or fanin) and not c_binary" > gpurun_out/pytest_$TAG.log 2>&1
+  -k "${TESTS_K:-(fifo or backlog or mute or hot or fanin) and not c_binary}" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
