@@ -509,7 +509,11 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "k_step", "kernel_ms": round(step_ms, 5),
+                # a two-pass table's step is two launches (zone_dev.h k_step PM
+                # 1 and 2); the events span both
+                "kernel": ("k_step" if os.environ.get("PONYC_AMD_SPLIT_PLAN") == "0"
+                           else "k_step<PINGER,1> + k_step<PINGER,2>"),
+                "kernel_ms": round(step_ms, 5),
                 "kernel_ms_source": "HIP events around the timed launches on the engine stream, / steps",
                 "alg_bytes_per_launch": round(alg_bytes, 1),
                 "lib_sha16": sha,

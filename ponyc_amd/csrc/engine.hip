@@ -372,6 +372,10 @@ struct Engine {
   uint64_t muted_on_cap = 0;
   uint32_t* d_ztrig[2] = {nullptr, nullptr};
   unsigned int* d_trig_n = nullptr;
+  // zones the step's two-pass launch ran (EngDev::zplan); split_plan: run a
+  // two-pass table's step as the two launches (PONYC_AMD_SPLIT_PLAN=0: one)
+  uint32_t* d_zplan = nullptr;
+  bool split_plan = true;
   uint32_t sidx = 0;
   // backlog copies handed to k_carry_big (EngDev::bigc)
   BigCopy* d_bigc = nullptr;
@@ -526,7 +530,10 @@ int upload_types()
   {
     const char* f = getenv("PONYC_AMD_TWO_PASS");
     e.two_pass = (f && atoi(f) == 0) ? 0u : 1u;
+    const char* sp = getenv("PONYC_AMD_SPLIT_PLAN");
+    g.split_plan = !(sp && atoi(sp) == 0);
   }
+  e.zplan = g.d_zplan;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -1348,13 +1355,20 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   // (five for an order-free zone's two passes: zone_dev.h two_pass)
   const size_t dyn = sizeof(uint32_t) * std::max<size_t>(5 * (g.n_zones + (R() > 1 ? R() : 0)),
                                                           se.sort_work);
-  step_kernel_t kern = se.kernel;
+  // a two-pass table's step as two launches: its two-pass zones, then the rest
+  // (zone_dev.h k_step PM)
+  const bool split = se.plan && g.split_plan;
+  step_kernel_t kern = split ? se.plan : se.kernel;
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
+    const bool more = split || g.defer_big;
     hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
-      e0, g.defer_big ? nullptr : e1, 0u, g.par, slot, g.sidx);
+      e0, more ? nullptr : e1, 0u, g.par, slot, g.sidx);
+    if(split)
+      hipExtLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
+        nullptr, g.defer_big ? nullptr : e1, 0u, g.par, slot, g.sidx);
     if(g.defer_big)
       hipExtLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream,
         nullptr, e1, 0u);
@@ -1362,6 +1376,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   else
   {
     hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
+    if(split)
+      hipLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
     if(g.defer_big)
       hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream);
   }
@@ -1464,6 +1480,7 @@ void free_all()
     if(g.d_trig_own[p]) (void)hipFree(g.d_trig_own[p]);
     if(g.d_ztrig[p]) (void)hipFree(g.d_ztrig[p]);
   }
+  if(g.d_zplan) (void)hipFree(g.d_zplan);
   if(g.d_muted_on) (void)hipFree(g.d_muted_on);
   if(g.d_trig_n) (void)hipFree(g.d_trig_n);
   if(g.d_bigc) (void)hipFree(g.d_bigc);
@@ -1612,6 +1629,8 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipHostMalloc(&g.h_sstat, sizeof(Engine::SpillStat), hipHostMallocDefault));
   memset(g.h_sstat, 0, sizeof(Engine::SpillStat));
   HIPCK(hipMalloc(&g.d_need, kMaxZones * sizeof(uint32_t)));
+  HIPCK(hipMalloc(&g.d_zplan, kMaxZones * sizeof(uint32_t)));
+  HIPCK(hipMemsetAsync(g.d_zplan, 0, kMaxZones * sizeof(uint32_t), g.stream));
   g.trig_bytes = (g.cfg.max_actors + 2 * 4096 + 7) & ~7ull;   // room for either zone size
   for(int p = 0; p < 2; ++p)
   {
@@ -1745,6 +1764,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
     g.d_ztrig[p] = nullptr;
     g.trig_stale[p] = false;
   }
+  g.d_zplan = nullptr;
   g.trig_bytes = 0; g.d_muted_on = nullptr; g.muted_on_cap = 0; g.d_trig_n = nullptr; g.sidx = 0;
   g.d_bigc = nullptr; g.d_bigc_n = nullptr; g.defer_big = false;
   g.d_sort_tmp = nullptr; g.sort_tmp_bytes = 0;

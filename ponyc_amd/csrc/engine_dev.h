@@ -199,6 +199,8 @@ struct EngDev {
   // order-free zones run their behaviours twice instead of through the outbox
   // (zone_dev.h two_pass; PONYC_AMD_TWO_PASS=0 turns it off for A/B runs)
   uint32_t two_pass, pad7;
+  // [n_zones] zones the step's two-pass launch ran (k_step PM 1 sets, PM 2 clears)
+  uint32_t* zplan;
 };
 
 
@@ -236,6 +238,23 @@ __device__ __forceinline__ int type_of_global(uint32_t id)
 __device__ __forceinline__ uint32_t zone_capacity(uint32_t z)
 {
   return c_eng.zcapz[z];
+}
+
+// The same for a wave-uniform z (a workgroup's own zone): the values read
+// through the table are uniform too, but the compiler cannot prove it and
+// would hold them — and the zone's buffer pointers built from them — in
+// vector registers, which the general drain spills (the outbox pointer was
+// reloaded from scratch at every send). readfirstlane puts them in SGPRs.
+__device__ __forceinline__ uint32_t zone_cap_s(uint32_t z)
+{
+  return __builtin_amdgcn_readfirstlane(c_eng.zcapz[z]);
+}
+
+__device__ __forceinline__ uint64_t zone_off_s(uint32_t z)
+{
+  const uint64_t o = c_eng.zoff[z];
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)o);
 }
 
 // zone of a local slot, and the slot within its zone (this engine's geometry)

@@ -11,13 +11,19 @@ namespace gpa {
 
 // A/B experiment builds (-DGPA_STEP_ONLY=<table>) compile one instantiation;
 // the others become stubs the host refuses to launch (GPU_ACTOR_EINVAL).
+// Two-pass tables also compile the step as two launches (zone_dev.h k_step PM).
 #if defined(GPA_STEP_ONLY) && (GPA_STEP_ONLY != GPA_STEP_HT)
 #define GPA_STEP_STUB 1
 template <int HT> __global__ void k_step_stub(uint32_t, uint32_t, uint32_t) {}
 template __global__ void k_step_stub<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
 #else
 #define GPA_STEP_STUB 0
-template __global__ void k_step<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
+template __global__ void k_step<GPA_STEP_HT, 0>(uint32_t, uint32_t, uint32_t);
+template <int HT, int PM> constexpr step_kernel_t split_kernel()
+{
+  if constexpr(HT >= 0 && two_pass<HT>()) return k_step<HT, PM>;
+  else return nullptr;
+}
 #endif
 
 namespace {
@@ -32,10 +38,11 @@ hipError_t step_upload(const void* types, const void* eng, hipStream_t s)
 
 #if GPA_STEP_STUB
 StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork }; }
+                                      (uint32_t)kZoneThreads, kSortWork, nullptr, nullptr }; }
 #else
-StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT>, step_upload, false, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork }; }
+StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT, 0>, step_upload, false, (uint32_t)kZoneBits,
+                                      (uint32_t)kZoneThreads, kSortWork,
+                                      split_kernel<GPA_STEP_HT, 1>(), split_kernel<GPA_STEP_HT, 2>() }; }
 #endif
 
 } // namespace gpa

@@ -549,8 +549,8 @@ template <class Acc>
 __device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, uint32_t z,
   uint32_t co, uint32_t nxt)
 {
-  ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
-  const uint32_t cap = zone_capacity(z);
+  ZRec* cout = c_eng.carry[nxt] + zone_off_s(z);
+  const uint32_t cap = zone_cap_s(z);
   for(uint32_t k = done; k < n; ++k)
   {
     const ZRec r = acc.rec(k);
@@ -1037,7 +1037,14 @@ struct TileCtx : ActorBase {
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
 // HTS >= 0: every serial actor of this engine runs handler table HTS (the host
 // checks), so only that table is compiled in; HTS < 0: any mix of tables.
-template <int HTS>
+// PM (two-pass tables): 0 every path in one kernel; or the step as two
+// launches, so that the two-pass path gets registers of its own (alone it
+// needs 99 VGPRs and spills none; beside the general path the kernel holds 128
+// and spills 22): PM 1 runs only the zones that take the two-pass path — every
+// other zone returns before it has written anything — and marks them in
+// c_eng.zplan; PM 2, launched right behind it, runs the rest (the general
+// path, as PM 0 would) and clears the marks.
+template <int HTS, int PM>
 __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
   uint32_t sidx)
 {
@@ -1072,6 +1079,17 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
   const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  static_assert(PM == 0 || (HTS >= 0 && two_pass<HTS>()), "split launches are for two-pass tables");
+  if constexpr(PM == 2)
+  {
+    const uint32_t ran = c_eng.zplan[z];
+    __syncthreads();                            // every wave has read the mark
+    if(ran)
+    {
+      if(tid == 0) c_eng.zplan[z] = 0u;
+      return;
+    }
+  }
   // One rank: a zone buffer overflowed into the spill list. The host grows the
   // zones and lands those records before another step runs; until then every
   // step is a no-op (spill_n[cur] is final for this launch; halt is set only
@@ -1082,7 +1100,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
                                           : (*c_eng.spill_flag != 0u);
   if(halt_now)
   {
-    if(z == 0 && tid == 0)
+    if(PM != 1 && z == 0 && tid == 0)
     {
       *c_eng.halt = 1u;
       c_eng.pend[pend_slot] = kPendSkipped;
@@ -1100,7 +1118,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t R = c_eng.nranks, me = c_eng.rank;
   const uint32_t nz = c_eng.n_zones;
   const uint32_t nb = nz + (R > 1 ? R : 0u);
-  const uint32_t cap = zone_capacity(z);
+  const uint32_t cap = zone_cap_s(z);
+  const uint64_t zo = zone_off_s(z);
   uint32_t* s_hist = s_dyn;
   uint32_t* s_base = s_dyn + nb;
 
@@ -1108,10 +1127,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // trigger muting after the last step (overloaded or muted); ztn = nonzero
   // bytes this zone left in trig_own[nxt] two steps ago. trig_n is indexed by
   // step mod 3: read this step's, add to the next's, clear the one after.
-  const uint32_t ztc = c_eng.ztrig[cur][z];
-  const uint32_t ztn = c_eng.ztrig[nxt][z];
-  const bool gate = c_eng.trig_n[sidx % 3u] != 0u;
-  if(z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+  // (the zone's own counters: uniform, held in SGPRs — zone_cap_s)
+  const uint32_t ztc = __builtin_amdgcn_readfirstlane(c_eng.ztrig[cur][z]);
+  const uint32_t ztn = __builtin_amdgcn_readfirstlane(c_eng.ztrig[nxt][z]);
+  const bool gate = __builtin_amdgcn_readfirstlane(c_eng.trig_n[sidx % 3u]) != 0u;
+  if(PM != 1 && z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+  if constexpr(PM == 1)
+    if(gate || ztc != 0u || c_eng.two_pass == 0u) return;
   uint8_t* const tb_out = c_eng.trig_own[nxt];
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
@@ -1121,10 +1143,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(0);
 
   // ---- 1. count --------------------------------------------------------------
-  const uint32_t nc = min(c_eng.carry_n[cur][z], cap);
-  const uint32_t nl = min(c_eng.land_n[cur][z], cap);
+  const uint32_t nc = min(__builtin_amdgcn_readfirstlane(c_eng.carry_n[cur][z]), cap);
+  const uint32_t nl = min(__builtin_amdgcn_readfirstlane(c_eng.land_n[cur][z]), cap);
   if(nc + nl == 0 && ztc == 0)
   {
+    if constexpr(PM == 1) return;
     // an idle zone (uniform: every thread read the same counters) has
     // nothing to count, run or send — the quiet tail of a run, or zones of
     // a sparse workload; it only clears trigger bytes it left two steps ago
@@ -1143,8 +1166,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   else
     for(uint32_t i = tid; i < kZone / 4; i += kZoneThreads)
       reinterpret_cast<uint32_t*>(s_tb)[i] = 0;
-  const ZRec* C = c_eng.carry[cur] + c_eng.zoff[z];
-  const ZRec* Ld = c_eng.land[cur] + c_eng.zoff[z];
+  const ZRec* C = c_eng.carry[cur] + zo;
+  const ZRec* Ld = c_eng.land[cur] + zo;
   const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
   // carried records counted apart (s_ccnt); landed ones in s_cnt.
   // Carried mail is sorted by actor (carry-out writes each actor's remainder
@@ -1198,13 +1221,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     if(L0 >= c_types[t].lfirst && L0 + nact <= c_types[t].lfirst + c_types[t].lcount)
       tz = (int)t;
   tz = __builtin_amdgcn_readfirstlane(tz);
+  if constexpr(PM == 1)
+    if(tz < 0) return;
   // A zone of a two-pass table that may take that path (no backpressure
   // anywhere, one type) loads its actors' state now, coalesced, so that the
   // loads land while the landing buffer is counted; dropped if it does not.
   constexpr int kPW = plan_words<HTS>();
   uint64_t st[kRounds][kPW];
   if constexpr(HTS >= 0 && two_pass<HTS>())
-    if(!gate && ztc == 0 && tz >= 0)
+    if(PM != 2 && !gate && ztc == 0 && tz >= 0)
     {
       const TypeDev& T = c_types[tz];
 #pragma unroll
@@ -1250,12 +1275,16 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
   __syncthreads();
   GPA_STAMP(1);
-  if(tid == 0)
-  {
-    if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
-    c_eng.carry_n[cur][z] = 0;
-    c_eng.land_n[cur][z] = 0;
-  }
+  auto take_mail = [&]() __attribute__((always_inline)) {
+    if(tid == 0)
+    {
+      if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
+      c_eng.carry_n[cur][z] = 0;
+      c_eng.land_n[cur][z] = 0;
+      if constexpr(PM == 1) c_eng.zplan[z] = 1u;
+    }
+  };
+  if constexpr(PM != 1) take_mail();
 
 
   // An order-free table (its behaviours ignore the message: the message-ubench
@@ -1298,9 +1327,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       // overflow again): the zone's messages, each sending at most one, are
       // fewer than seq_max
       if constexpr(two_pass<HTS>())
-        plan = fast && s_tot < c_eng.seq_max && c_eng.two_pass != 0u;
+        plan = PM != 2 && fast && s_tot < c_eng.seq_max && c_eng.two_pass != 0u;
     }
-  ZRec* Sz = c_eng.S + 3 * c_eng.zoff[z];
+  if constexpr(PM == 1)
+  {
+    if(!plan) return;                           // uniform: left to PM 2
+    take_mail();
+  }
+  ZRec* Sz = c_eng.S + 3 * zo;
   // S path: the sorted items of the groups the workgroup sorted, each at its
   // segment offset (S's last third, 2 cap items; read by the drain, the
   // carry-out and k_carry_big)
@@ -1425,7 +1459,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     const uint32_t nbig = min(s_nbig, kMaxBig);     // past kMaxBig: the lane sorts (slow, exact)
     if(nbig)
     {
-      uint64_t* ia = reinterpret_cast<uint64_t*>(c_eng.O + c_eng.zoff[z]);
+      uint64_t* ia = reinterpret_cast<uint64_t*>(c_eng.O + zo);
       for(uint32_t k = 0; k < nbig; ++k)
       {
         const uint32_t i = s_big[k];
@@ -1677,14 +1711,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       xover += tc.xover;
       if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
     }
-  if(!plan)
+  if(PM != 1 && !plan)
   {
   // s_aux will hold each actor's unhandled remainder (known after it ran)
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   int any_rem = 0;
 
   // ---- 3. run handlers -------------------------------------------------------------
-  a.out = c_eng.O + c_eng.zoff[z];
+  a.out = c_eng.O + zo;
   a.s_nout = &s_nout;
   a.ocap = cap;
   a.nxt = nxt;
@@ -1823,7 +1857,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t co = s_aux[i];
       const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
       const uint32_t n = s_cnt[i];
-      ZRec* cout = c_eng.carry[nxt] + c_eng.zoff[z];
+      ZRec* cout = c_eng.carry[nxt] + zo;
       if(c_eng.defer_big && !use_idx && co + rem <= cap)
       {
         // listed for k_carry_big, which copies it with every CU right after
@@ -1931,7 +1965,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
-  if(!plan)
+  if(PM != 1 && !plan)
   {
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile
@@ -1955,7 +1989,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // than 64 records to 64 chunks (measured 1.75x for a whole-zone sort,
   // scripts/ubench_scatter.hip).
   const uint32_t nout = min(s_nout, cap);
-  const ORec* Oz = c_eng.O + c_eng.zoff[z];
+  const ORec* Oz = c_eng.O + zo;
   // r = {to, w, arg lo, arg hi} -> position pos of bucket b's chunk
   auto emit = [&](const uint4& r, uint32_t b, uint32_t pos) __attribute__((always_inline)) {
     xover += emit_rec(r, b, pos, L0, nz, nxt);
