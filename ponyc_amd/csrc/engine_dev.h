@@ -199,7 +199,7 @@ struct EngDev {
   // order-free zones run their behaviours twice instead of through the outbox
   // (zone_dev.h two_pass; PONYC_AMD_TWO_PASS=0 turns it off for A/B runs)
   uint32_t two_pass, pad7;
-  // [n_zones] zones the step's two-pass launch ran (k_step PM 1 sets, PM 2 clears)
+  // [n_zones] zones the step's two-pass launch ran: step index + 1 (k_step PM 1)
   uint32_t* zplan;
 };
 

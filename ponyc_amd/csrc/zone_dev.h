@@ -545,12 +545,12 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
 // The unhandled tail [done, n) of an actor's segment, already canonical, to
 // the next step's carry buffer at carry position co (positions past the
 // zone's capacity go to the spill list: never lost).
-template <class Acc>
+template <bool SR, class Acc>
 __device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, uint32_t z,
   uint32_t co, uint32_t nxt)
 {
-  ZRec* cout = c_eng.carry[nxt] + zone_off_s(z);
-  const uint32_t cap = zone_cap_s(z);
+  ZRec* cout = c_eng.carry[nxt] + (SR ? zone_off_s(z) : c_eng.zoff[z]);
+  const uint32_t cap = SR ? zone_cap_s(z) : zone_capacity(z);
   for(uint32_t k = done; k < n; ++k)
   {
     const ZRec r = acc.rec(k);
@@ -1043,7 +1043,7 @@ struct TileCtx : ActorBase {
 // and spills 22): PM 1 runs only the zones that take the two-pass path — every
 // other zone returns before it has written anything — and marks them in
 // c_eng.zplan; PM 2, launched right behind it, runs the rest (the general
-// path, as PM 0 would) and clears the marks.
+// path, as PM 0 would).
 template <int HTS, int PM>
 __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
   uint32_t sidx)
@@ -1080,16 +1080,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 
   const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   static_assert(PM == 0 || (HTS >= 0 && two_pass<HTS>()), "split launches are for two-pass tables");
+  // (the mark is the step's index + 1: nothing clears it, and a step that
+  // halted — and runs again with the same index — marked no zone)
   if constexpr(PM == 2)
-  {
-    const uint32_t ran = c_eng.zplan[z];
-    __syncthreads();                            // every wave has read the mark
-    if(ran)
-    {
-      if(tid == 0) c_eng.zplan[z] = 0u;
-      return;
-    }
-  }
+    if(__builtin_amdgcn_readfirstlane(c_eng.zplan[z]) == sidx + 1u) return;
   // One rank: a zone buffer overflowed into the spill list. The host grows the
   // zones and lands those records before another step runs; until then every
   // step is a no-op (spill_n[cur] is final for this launch; halt is set only
@@ -1118,8 +1112,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t R = c_eng.nranks, me = c_eng.rank;
   const uint32_t nz = c_eng.n_zones;
   const uint32_t nb = nz + (R > 1 ? R : 0u);
-  const uint32_t cap = zone_cap_s(z);
-  const uint64_t zo = zone_off_s(z);
+  // The zone's offset, capacity and counters through SGPRs (zone_cap_s):
+  // measured faster for the pinger (C2) and the storm, slower for C2-det,
+  // whose kernel then spills more SGPRs (profiles/r04y_split_sgpr_ab.txt)
+  constexpr bool SR = HTS != GPU_ACTOR_HT_PINGER_DET;
+  auto rfl = [](uint32_t v) __attribute__((always_inline)) {
+    return SR ? __builtin_amdgcn_readfirstlane(v) : v;
+  };
+  const uint32_t cap = SR ? zone_cap_s(z) : zone_capacity(z);
+  const uint64_t zo = SR ? zone_off_s(z) : c_eng.zoff[z];
   uint32_t* s_hist = s_dyn;
   uint32_t* s_base = s_dyn + nb;
 
@@ -1127,10 +1128,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // trigger muting after the last step (overloaded or muted); ztn = nonzero
   // bytes this zone left in trig_own[nxt] two steps ago. trig_n is indexed by
   // step mod 3: read this step's, add to the next's, clear the one after.
-  // (the zone's own counters: uniform, held in SGPRs — zone_cap_s)
-  const uint32_t ztc = __builtin_amdgcn_readfirstlane(c_eng.ztrig[cur][z]);
-  const uint32_t ztn = __builtin_amdgcn_readfirstlane(c_eng.ztrig[nxt][z]);
-  const bool gate = __builtin_amdgcn_readfirstlane(c_eng.trig_n[sidx % 3u]) != 0u;
+  const uint32_t ztc = rfl(c_eng.ztrig[cur][z]);
+  const uint32_t ztn = rfl(c_eng.ztrig[nxt][z]);
+  const bool gate = rfl(c_eng.trig_n[sidx % 3u]) != 0u;
   if(PM != 1 && z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
   if constexpr(PM == 1)
     if(gate || ztc != 0u || c_eng.two_pass == 0u) return;
@@ -1143,8 +1143,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   GPA_STAMP(0);
 
   // ---- 1. count --------------------------------------------------------------
-  const uint32_t nc = min(__builtin_amdgcn_readfirstlane(c_eng.carry_n[cur][z]), cap);
-  const uint32_t nl = min(__builtin_amdgcn_readfirstlane(c_eng.land_n[cur][z]), cap);
+  const uint32_t nc = min(rfl(c_eng.carry_n[cur][z]), cap);
+  const uint32_t nl = min(rfl(c_eng.land_n[cur][z]), cap);
   if(nc + nl == 0 && ztc == 0)
   {
     if constexpr(PM == 1) return;
@@ -1281,7 +1281,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
       c_eng.carry_n[cur][z] = 0;
       c_eng.land_n[cur][z] = 0;
-      if constexpr(PM == 1) c_eng.zplan[z] = 1u;
+      if constexpr(PM == 1) c_eng.zplan[z] = sidx + 1u;
     }
   };
   if constexpr(PM != 1) take_mail();
@@ -1845,9 +1845,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       }
       const uint32_t n = s_cnt[i];
       if(use_idx)
-        carry_out(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
+        carry_out<SR>(AccIdx{s_idx + s_off[i], C, Ld, nc}, n - rem, n, z, co, nxt);
       else
-        carry_out(acc_s(i), n - rem, n, z, co, nxt);
+        carry_out<SR>(acc_s(i), n - rem, n, z, co, nxt);
     }
     __syncthreads();
     const uint32_t nbig = min(s_nbig, kMaxBig);

@@ -5,5 +5,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 RUNS="mono|ponyc_amd/variants/split/libgpuactor.so|PONYC_AMD_SPLIT_PLAN=0|pinger det storm;new|ponyc_amd/libgpuactor.so||pinger det storm" \
-  REPS=2 TAG=y bash scripts/gpu_stage_ab.sh || exit $?
-PART=A TAG=r04y bash scripts/gpu_evidence.sh
+  REPS=2 TAG=${ABTAG:-y} bash scripts/gpu_stage_ab.sh || exit $?
+PART=A TAG=${EVTAG:-r04y} bash scripts/gpu_evidence.sh
