@@ -19,9 +19,12 @@ template __global__ void k_step_stub<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
 #else
 #define GPA_STEP_STUB 0
 template __global__ void k_step<GPA_STEP_HT, 0>(uint32_t, uint32_t, uint32_t);
+// split for the two-pass table and for the general-path tables whose plain
+// zones spill least without the cold paths (measured: C2-det, the storm)
 template <int HT, int PM> constexpr step_kernel_t split_kernel()
 {
-  if constexpr(HT >= 0 && two_pass<HT>()) return k_step<HT, PM>;
+  if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM))
+    return k_step<HT, PM>;
   else return nullptr;
 }
 #endif

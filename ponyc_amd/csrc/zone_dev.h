@@ -1079,7 +1079,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
   const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  static_assert(PM == 0 || (HTS >= 0 && two_pass<HTS>()), "split launches are for two-pass tables");
+  static_assert(PM == 0 || HTS >= 0, "split launches are for one-table engines");
+  // PM 1 of a two-pass table takes the zones that plan; of any other table
+  // the plain zones (kSimple): no backpressure, no carried mail, the LDS
+  // index, no group over kBigGroup — the drain without the scratch path, the
+  // hot-group sort and the mute checks, which then need no registers
+  constexpr bool kPlanSplit = HTS >= 0 && two_pass<HTS>();
+  constexpr bool kSimple = PM == 1 && !kPlanSplit;
   // (the mark is the step's index + 1: nothing clears it, and a step that
   // halted — and runs again with the same index — marked no zone)
   if constexpr(PM == 2)
@@ -1133,7 +1139,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const bool gate = rfl(c_eng.trig_n[sidx % 3u]) != 0u;
   if(PM != 1 && z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
   if constexpr(PM == 1)
-    if(gate || ztc != 0u || c_eng.two_pass == 0u) return;
+    if(gate || ztc != 0u || (kPlanSplit && c_eng.two_pass == 0u)) return;
   uint8_t* const tb_out = c_eng.trig_own[nxt];
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
@@ -1159,6 +1165,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
     return;
   }
+  if constexpr(kSimple)
+    if(nc != 0u || nl > kIdxCap) return;
   // the trigger bytes of this zone's actors as the last step left them
   if(ztc)
     for(uint32_t i = tid; i < kZone; i += kZoneThreads)
@@ -1168,7 +1176,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       reinterpret_cast<uint32_t*>(s_tb)[i] = 0;
   const ZRec* C = c_eng.carry[cur] + zo;
   const ZRec* Ld = c_eng.land[cur] + zo;
-  const bool use_idx = nc + nl <= kIdxCap;       // uniform per workgroup
+  const bool use_idx = kSimple || nc + nl <= kIdxCap;       // uniform per workgroup
   // carried records counted apart (s_ccnt); landed ones in s_cnt.
   // Carried mail is sorted by actor (carry-out writes each actor's remainder
   // at its scan offset). A large carry (a backlog) is counted from samples:
@@ -1178,7 +1186,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // Elsewhere a wave's lanes mostly share one counter, folded into one atomic.
   uint32_t nmix = 0;
   const uint32_t nrun = (nc + kCarryRun - 1) / kCarryRun;
-  const bool sampled = nc > kIdxCap && nrun <= kIdxCap / 2;     // uniform
+  const bool sampled = !kSimple && nc > kIdxCap && nrun <= kIdxCap / 2;     // uniform
   uint32_t* const s_mix = reinterpret_cast<uint32_t*>(s_idx);
   if(sampled)
   {
@@ -1331,7 +1339,16 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
   if constexpr(PM == 1)
   {
-    if(!plan) return;                           // uniform: left to PM 2
+    if constexpr(kPlanSplit)
+    {
+      if(!plan) return;                         // uniform: left to PM 2
+    }
+    else
+    {
+      int big = 0;
+      for(uint32_t i = tid; i < kZone; i += kZoneThreads) big |= s_cnt[i] > kBigGroup;
+      if(__syncthreads_or(big)) return;         // a hot group: left to PM 2
+    }
     take_mail();
   }
   ZRec* Sz = c_eng.S + 3 * zo;
@@ -1456,7 +1473,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
   __syncthreads();
   {
-    const uint32_t nbig = min(s_nbig, kMaxBig);     // past kMaxBig: the lane sorts (slow, exact)
+    const uint32_t nbig = kSimple ? 0u : min(s_nbig, kMaxBig);     // past kMaxBig: the lane sorts (slow, exact)
     if(nbig)
     {
       uint64_t* ia = reinterpret_cast<uint64_t*>(c_eng.O + zo);
@@ -1480,7 +1497,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }   // general path
   GPA_STAMP(7);                          // diagnostic build: the hot-group sort ends
   auto big_sorted = [&](uint32_t i) __attribute__((always_inline)) {
-    return ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
+    return !kSimple && ((s_bigbits[i >> 5] >> (i & 31)) & 1u) != 0u;
   };
   // S path accessor of actor i (a group the workgroup sorted: read through its items)
   auto acc_s = [&](uint32_t i) __attribute__((always_inline)) {
@@ -1711,7 +1728,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       xover += tc.xover;
       if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
     }
-  if(PM != 1 && !plan)
+  if(!(PM == 1 && kPlanSplit) && !plan)
   {
   // s_aux will hold each actor's unhandled remainder (known after it ran)
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
@@ -1732,7 +1749,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       if(a.fan_t >= 0) a.fan = s_fan;
     }
   // drain local actor i, of type t (T = c_types[t])
-  uint8_t* const trig_cur = gate ? c_eng.trig[cur] : nullptr;
+  uint8_t* const trig_cur = (!kSimple && gate) ? c_eng.trig[cur] : nullptr;
   auto drain_actor = [&](const TypeDev& T, int t, uint32_t i) __attribute__((always_inline)) {
     const uint32_t n = s_cnt[i];
     const uint32_t L = L0 + i;
@@ -1837,7 +1854,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       const uint32_t co = s_aux[i];
       const uint32_t rem = (i + 1 < kZone ? s_aux[i + 1] : ncout) - co;
       if(rem == 0) continue;
-      if(rem > kBigGroup)
+      if(!kSimple && rem > kBigGroup)       // (kSimple: no group over kBigGroup)
       {
         // a backlog (an overloaded receiver): copied by the whole workgroup
         const uint32_t k = atomicAdd(&s_nbig, 1u);
@@ -1965,7 +1982,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
-  if(PM != 1 && !plan)
+  if(!(PM == 1 && kPlanSplit) && !plan)
   {
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile

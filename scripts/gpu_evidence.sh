@@ -13,11 +13,13 @@ export TMPDIR=/tmp
 TAG=${TAG:-r04}
 mkdir -p gpurun_out/prof
 if [ -z "$PART" ] || [ "$PART" = A ]; then
-  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread \
-    > gpurun_out/pytest_gpu_$TAG.log 2>&1
-  rc=$?
-  echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_$TAG.log
-  [ $rc -eq 0 ] || exit $rc
+  if [ -z "$SKIP_PYTEST" ]; then      # (SKIP_PYTEST=1: the caller ran the suite)
+    timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread \
+      > gpurun_out/pytest_gpu_$TAG.log 2>&1
+    rc=$?
+    echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_$TAG.log
+    [ $rc -eq 0 ] || exit $rc
+  fi
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
   tail -3 gpurun_out/smoke_$TAG.log
   if [ -z "$SKIP_FULL_BENCH" ]; then
