@@ -683,6 +683,13 @@ int or_state_write(uint32_t type_id, uint64_t first, uint64_t n, const uint64_t*
   return 0;
 }
 
+/* Actors whose trigger byte the last step left nonzero (overloaded or muted):
+ * the oracle's side of the engine's per-step trigger count (trig_n). */
+uint64_t or_trig_count(void)
+{
+  return S.init ? S.n_trig : 0;
+}
+
 int or_counts(uint64_t* out)
 {
   out[0] = S.steps;

@@ -38,8 +38,19 @@ static void analyzer_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m
   analyzer_t* a = (analyzer_t*)self;
   a->msgs_received += 1;                                   /* main.pony:219-220 */
   a->acc ^= (uint64_t)((pony_msgi_t*)m)->i;
+}
+
+static void analyzer_out(const analyzer_t* a)
+{
   g_count[a->idx] = a->msgs_received;
   g_acc[a->idx] = a->acc;
+}
+
+static void analyzer_final(void* self)
+{
+  const analyzer_t* a = (const analyzer_t*)self;
+  analyzer_out(a);
+  h_fin[a->idx] = 1;
 }
 
 static void sender_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
@@ -55,7 +66,8 @@ static void sender_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
     pony_send(ctx, self, SEND_MSGS);
 }
 
-static pony_type_t analyzer_type = { .id = 3, .size = sizeof(analyzer_t), .dispatch = analyzer_dispatch };
+static pony_type_t analyzer_type = { .id = 3, .size = sizeof(analyzer_t), .dispatch = analyzer_dispatch,
+  .final = analyzer_final };
 static pony_type_t sender_type = { .id = 4, .size = sizeof(sender_t), .dispatch = sender_dispatch };
 
 int main(int argc, char** argv)
@@ -70,6 +82,7 @@ int main(int argc, char** argv)
 
   g_an = calloc(g_na, sizeof(analyzer_t*));
   g_count = calloc(g_na, 8); g_acc = calloc(g_na, 8);
+  h_fin = calloc(g_na, 1);
 
   pony_ctx_t* ctx = h_start(threads, noscale);
   for(uint64_t i = 0; i < g_na; i++)
@@ -90,6 +103,8 @@ int main(int argc, char** argv)
   }
 
   double secs = h_run(ctx);
+  for(uint64_t i = 0; i < g_na; i++)
+    if(!h_fin[i]) analyzer_out(g_an[i]);
 
   uint64_t total = 0;
   for(uint64_t i = 0; i < g_na; i++) total += g_count[i];

@@ -39,7 +39,20 @@ static void sink_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
   k->h = (k->h ^ arg) * 0x100000001b3ULL;
   if(seq != k->last[slot] + 1) k->bad += 1;
   k->last[slot] = seq;
+}
+
+static sink_t** g_sinks;
+
+static void sink_out(const sink_t* k)
+{
   g_h[k->idx] = k->h; g_n[k->idx] = k->n; g_bad[k->idx] = k->bad;
+}
+
+static void sink_final(void* self)
+{
+  const sink_t* k = (const sink_t*)self;
+  sink_out(k);
+  h_fin[k->idx] = 1;
 }
 
 static void src_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
@@ -56,7 +69,8 @@ static void src_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
     pony_sendi(ctx, self, BURST, burst);
 }
 
-static pony_type_t sink_type = { .id = 7, .size = sizeof(sink_t), .dispatch = sink_dispatch };
+static pony_type_t sink_type = { .id = 7, .size = sizeof(sink_t), .dispatch = sink_dispatch,
+  .final = sink_final };
 static pony_type_t src_type = { .id = 8, .size = sizeof(src_t), .dispatch = src_dispatch };
 
 int main(int argc, char** argv)
@@ -71,6 +85,8 @@ int main(int argc, char** argv)
 
   g_h = calloc(g_nsinks, 8); g_n = calloc(g_nsinks, 8); g_bad = calloc(g_nsinks, 8);
   sink_t** sinks = calloc(g_nsinks, sizeof(sink_t*));
+  g_sinks = sinks;
+  h_fin = calloc(g_nsinks, 1);
 
   pony_ctx_t* ctx = h_start(threads, noscale);
   for(uint64_t k = 0; k < g_nsinks; k++)
@@ -78,7 +94,6 @@ int main(int argc, char** argv)
     sink_t* s = (sink_t*)pony_create(ctx, &sink_type);
     s->h = 0xcbf29ce484222325ULL;
     s->idx = k;
-    g_h[k] = s->h;
     sinks[k] = s;
   }
   for(uint64_t i = 0; i < nsrc; i++)
@@ -92,6 +107,8 @@ int main(int argc, char** argv)
   }
 
   double secs = h_run(ctx);
+  for(uint64_t k = 0; k < g_nsinks; k++)
+    if(!h_fin[k]) sink_out(g_sinks[k]);
 
   uint64_t total = 0;
   for(uint64_t k = 0; k < g_nsinks; k++) total += g_n[k];

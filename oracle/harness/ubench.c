@@ -60,7 +60,6 @@ static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
       uint64_t k = or_rand_int(&p->rand, g_n);         /* _rand.int(_num_ps) */
       pony_sendi(ctx, (pony_actor_t*)g_ps[k], PING, 42);
     }
-    g_x[p->idx] = p->rand.x; g_y[p->idx] = p->rand.y; g_count[p->idx] = p->count;
   } else {
     p->count += 1;
     p->acc ^= payload;
@@ -71,18 +70,33 @@ static void pinger_dispatch(pony_ctx_t* ctx, pony_actor_t* self, pony_msg_t* m)
       pony_sendi(ctx, (pony_actor_t*)g_ps[k], PING,
         (intptr_t)((payload & 0xFFFFFFFF00000000ULL) | (hop + 1)));
     }
-    g_count[p->idx] = p->count; g_acc[p->idx] = p->acc;
   }
 }
 
-static pony_type_t pinger_type = { .id = 2, .size = sizeof(pinger_t), .dispatch = pinger_dispatch };
+/* a pinger's state to the output arrays (its finaliser, or after the run) */
+static void pinger_out(const pinger_t* p)
+{
+  g_x[p->idx] = p->rand.x; g_y[p->idx] = p->rand.y;
+  g_count[p->idx] = p->count; g_acc[p->idx] = p->acc;
+}
 
-/* pings handled so far: the pingers' counts, read while they run (each word
- * is written by its own pinger; a read may be one ping stale) */
+static void pinger_final(void* self)
+{
+  const pinger_t* p = (const pinger_t*)self;
+  pinger_out(p);
+  h_fin[p->idx] = 1;
+}
+
+static pony_type_t pinger_type = { .id = 2, .size = sizeof(pinger_t), .dispatch = pinger_dispatch,
+  .final = pinger_final };
+
+/* pings handled so far: the pingers' counts, read in the live actors while
+ * they run (rc = GC_INC_MORE: none is reaped during the run; each word is
+ * written by its own pinger, and a read may be one ping stale) */
 static uint64_t count_sum(void)
 {
   uint64_t s = 0;
-  for(uint64_t i = 0; i < g_n; i++) s += __atomic_load_n(&g_count[i], __ATOMIC_RELAXED);
+  for(uint64_t i = 0; i < g_n; i++) s += __atomic_load_n(&g_ps[i]->count, __ATOMIC_RELAXED);
   return s;
 }
 
@@ -118,6 +132,7 @@ int main(int argc, char** argv)
 
   g_ps = calloc(g_n, sizeof(pinger_t*));
   g_x = calloc(g_n, 8); g_y = calloc(g_n, 8); g_count = calloc(g_n, 8); g_acc = calloc(g_n, 8);
+  h_fin = calloc(g_n, 1);
 
   pony_ctx_t* ctx = h_start(threads, noscale);
 
@@ -133,7 +148,6 @@ int main(int argc, char** argv)
       (void)or_rand_int(&p->rand, 100);
       (void)or_rand_int(&p->rand, 100);
       (void)or_rand_int(&p->rand, 100);
-      g_x[i] = p->rand.x; g_y[i] = p->rand.y;
     }
     g_ps[i] = p;
   }
@@ -150,6 +164,8 @@ int main(int argc, char** argv)
   if(windowed) pthread_create(&timer, NULL, window_timer, NULL);
   double secs = h_run(ctx);
   if(windowed) pthread_join(timer, NULL);
+  for(uint64_t i = 0; i < g_n; i++)
+    if(!h_fin[i]) pinger_out(g_ps[i]);
 
   uint64_t total = 0;
   for(uint64_t i = 0; i < g_n; i++) total += g_count[i];

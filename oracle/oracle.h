@@ -71,6 +71,7 @@ int  or_run(uint64_t max_steps, uint64_t* steps_done);
 int  or_state_read(uint32_t type_id, uint64_t first, uint64_t n, uint64_t* out);
 int  or_state_write(uint32_t type_id, uint64_t first, uint64_t n, const uint64_t* in);
 /* counts: [0]=steps [1]=delivered [2]=sent [3]=pending [4]=dropped */
+uint64_t or_trig_count(void);
 int  or_counts(uint64_t* out5);
 int  or_type_delivered(uint32_t type_id, uint64_t* out);
 

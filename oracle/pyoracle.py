@@ -158,6 +158,12 @@ class Oracle:
         _ck("or_state_write", self.lib.or_state_write(type_id, first, arr.shape[1],
                                                       arr.ctypes.data_as(ctypes.c_void_p)))
 
+    def trig_count(self) -> int:
+        """Actors the last step left overloaded or muted."""
+        fn = self.lib.or_trig_count
+        fn.restype = ctypes.c_uint64
+        return int(fn())
+
     def counts(self):
         c = (ctypes.c_uint64 * 5)()
         self.lib.or_counts(c)

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <atomic>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -213,7 +214,9 @@ __global__ void __launch_bounds__(kBlock) k_carry_big()
   const unsigned long long v = c_eng.bigc_n[0];   // final: k_step ran to completion before
   const uint32_t n = min((uint32_t)(v >> 32), c_eng.bigc_cap);
   if(n == 0) return;
-  const uint32_t total = (uint32_t)v;
+  // the listed copies' records: the last one's base + its length (bigc_n's
+  // low word also counts copies past bigc_cap, which their zones made)
+  const uint32_t total = c_eng.bigc[n - 1].base + c_eng.bigc[n - 1].rem;
   const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
   const uint32_t c0 = blockIdx.x * per, c1 = min(c0 + per, total);
   if(c0 < c1)
@@ -308,6 +311,8 @@ struct Engine {
   uint32_t par = 0;                     // parity the next step reads
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_pend = nullptr;
+  unsigned long long* d_pend_sh = nullptr;    // [kPendSlots][kShards]: k_step's adds
+  unsigned long long* d_stats_sh = nullptr;   // [ST_COUNT][kShards]
   unsigned long long* d_dbg = nullptr;   // phase stamps of the diagnostic build
   gpu_msg_t* h_msgs = nullptr; uint64_t h_msgs_cap = 0;
   // gpu_actor_send appends here; flushed (one H2D + k_inject) before the
@@ -503,6 +508,7 @@ int upload_types()
   }
   e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
+  e.pend_sh = g.d_pend_sh; e.stats_sh = g.d_stats_sh;
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
   e.seq_max = R() > 1 ? kXSeqMax : kSeqMax;
   e.dbg = g.d_dbg;
@@ -558,7 +564,9 @@ int ensure_spill(uint64_t cap)
   return 0;
 }
 
-int relayout_zones();
+int relayout_zones(bool geometry = false);
+StepEntry step_entry_for(bool z12);
+bool step_fits(const StepEntry& se, uint64_t nb);
 int upload_types();
 int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out);
 
@@ -671,7 +679,10 @@ uint32_t pick_zone_bits(uint64_t n)
   const uint64_t nz11 = (n + 2047) / 2048, nz12 = (n + 4095) / 4096;
   if(const char* f = getenv("PONYC_AMD_ZONE_BITS"))      // test hook: force a geometry
     return atoi(f) == 12 ? 12u : 11u;
-  return (nz11 + rb > 640 && nz12 + rb <= 2300) ? 12u : 11u;
+  // 4096-actor zones while their bucket arrays fit the LDS beside the z12
+  // kernels' static LDS (~2,200 buckets; ~1,500 for the two-pass table's six
+  // arrays); past that, 2048-actor zones at one workgroup per CU
+  return (nz11 + rb > 640 && step_fits(step_entry_for(true), nz12 + rb)) ? 12u : 11u;
 }
 
 // No mail anywhere (landing or carried, either parity): a geometry change
@@ -691,7 +702,10 @@ bool zones_empty()
   return true;
 }
 
-int relayout_zones()
+// geometry: the zone geometry may be re-chosen (gpu_actor_create only: every
+// rank creates alike, so the collective below is reached by all of them; a
+// spill fixup can run on one rank alone and keeps the geometry).
+int relayout_zones(bool geometry)
 {
   // the geometry may change only before any step ran, with no mail landed
   // (zone buffers are copied zone by zone below)
@@ -703,7 +717,7 @@ int relayout_zones()
   bool fresh = false;
   {
     const uint32_t want = pick_zone_bits((g.n_actors + R() - 1) / R());
-    if(want != g.zbits && g.steps_total == 0 && g.sparse_launches == 0)
+    if(geometry && want != g.zbits && g.steps_total == 0 && g.sparse_launches == 0)
     {
       HIPCK(hipStreamSynchronize(g.stream));
       bool empty = zones_empty();
@@ -840,9 +854,52 @@ uint32_t required_words(uint32_t ht)
   }
 }
 
+// Sum the sharded per-step counters of k_step (EngDev::pend_sh / stats_sh)
+// into pend[first, first + n) and stats[], and clear the shards. One block;
+// stream-ordered behind the steps, so plain adds.
+__global__ void __launch_bounds__(kBlock) k_fold(uint32_t first, uint32_t n)
+{
+  for(uint32_t s = first + threadIdx.x; s < first + n; s += kBlock)
+  {
+    unsigned long long* sh = c_eng.pend_sh + (size_t)s * kShards;
+    unsigned long long v = 0;
+    for(uint32_t k = 0; k < kShards; ++k) { v += sh[k]; sh[k] = 0; }
+    if(v) c_eng.pend[s] += v;
+  }
+  for(uint32_t i = threadIdx.x; i < ST_COUNT; i += kBlock)
+  {
+    unsigned long long* sh = c_eng.stats_sh + (size_t)i * kShards;
+    unsigned long long v = 0;
+    for(uint32_t k = 0; k < kShards; ++k) { v += sh[k]; sh[k] = 0; }
+    if(v) c_eng.stats[i] += v;
+  }
+}
+
+// k_step's sharded counters folded into pend[first, first + n) and stats[]
+// (n == 0: stats only), ahead of a host read of either.
+int fold_counters(uint32_t first, uint32_t n)
+{
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(kBlock), 0, g.stream, first, n);
+  HIPCK(hipGetLastError());
+  return 0;
+}
+
+// Zero pend[first, first + n) and their shards.
+int pend_clear(uint32_t first, uint32_t n)
+{
+  HIPCK(hipMemsetAsync(g.d_pend + first, 0, n * sizeof(unsigned long long), g.stream));
+  HIPCK(hipMemsetAsync(g.d_pend_sh + (size_t)first * kShards, 0,
+    (size_t)n * kShards * sizeof(unsigned long long), g.stream));
+  return 0;
+}
+
 int check_sticky()
 {
   unsigned long long st[ST_COUNT];
+  {
+    const int rc = fold_counters(0, 0);
+    if(rc) return rc;
+  }
   HIPCK(hipMemcpyAsync(st, g.d_stats, sizeof(st), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   if(st[ST_DROPPED] || st[ST_XCHG_OVERFLOW]) g.sticky = GPU_ACTOR_EMAILBOX;
@@ -1210,7 +1267,7 @@ int exchange_step(uint32_t step_sidx)
 
 // k_step compiled for the one handler table all serial actors share, when
 // they do (smaller code, no spills); the any-mix instantiation otherwise.
-StepEntry pick_step_entry()
+StepEntry step_entry_for(bool z12)
 {
   int only = -1;
   bool mixed = false;
@@ -1221,7 +1278,6 @@ StepEntry pick_step_entry()
     only = (int)t.ht;
   }
   if(mixed) only = -1;
-  const bool z12 = g.zbits == 12;
   switch(only)
   {
     case GPU_ACTOR_HT_RING: return z12 ? gpa_z12::step_entry_ring() : gpa::step_entry_ring();
@@ -1236,6 +1292,41 @@ StepEntry pick_step_entry()
     case GPU_ACTOR_HT_SPREADER: return z12 ? gpa_z12::step_entry_spreader() : gpa::step_entry_spreader();
     default: return z12 ? gpa_z12::step_entry_any() : gpa::step_entry_any();
   }
+}
+
+StepEntry pick_step_entry() { return step_entry_for(g.zbits == 12); }
+
+// LDS a workgroup may hold on gfx950 (the CU's whole 160 KB; two 512-thread
+// zones per CU at <= 80 KB each)
+constexpr size_t kLdsPerWorkgroup = 160 * 1024;
+
+// Dynamic LDS of a step launch with nb destination buckets: the bucket
+// arrays (zone_dev.h: histogram, chunk bases, tile counts, tile starts, and
+// the two-pass table's round counts) or the hot-group sort's work area.
+size_t step_dyn_bytes(const StepEntry& se, uint64_t nb)
+{
+  return sizeof(uint32_t) * std::max<uint64_t>((uint64_t)se.bucket_words * nb, se.sort_work);
+}
+
+// Whether a step launch with nb buckets fits a workgroup's LDS: static LDS of
+// every kernel of the entry (hipFuncGetAttributes) + the dynamic part.
+bool step_fits(const StepEntry& se, uint64_t nb)
+{
+  static std::map<step_kernel_t, size_t> cache;     // (callers hold g.mu)
+  size_t st = 0;
+  for(step_kernel_t k : {se.kernel, se.plan, se.rest})
+  {
+    if(!k) continue;
+    auto it = cache.find(k);
+    if(it == cache.end())
+    {
+      hipFuncAttributes a;
+      if(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k)) != hipSuccess) return false;
+      it = cache.emplace(k, a.sharedSizeBytes).first;
+    }
+    st = std::max<size_t>(st, it->second);
+  }
+  return st + step_dyn_bytes(se, nb) <= kLdsPerWorkgroup;
 }
 
 // Ids and landing for the actors the last step's behaviours created: the
@@ -1351,10 +1442,11 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   if(g.n_zones == 0) return 0;
   const StepEntry se = pick_step_entry();
   if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
-  // bucket arrays (4 x buckets) and, for hot receivers, the sort's work area
-  // (five for an order-free zone's two passes: zone_dev.h two_pass)
-  const size_t dyn = sizeof(uint32_t) * std::max<size_t>(5 * (g.n_zones + (R() > 1 ? R() : 0)),
-                                                          se.sort_work);
+  // bucket arrays (4 x buckets; six for an order-free zone's two passes:
+  // zone_dev.h two_pass) and, for hot receivers, the sort's work area
+  const uint64_t nb = g.n_zones + (R() > 1 ? R() : 0);
+  if(!step_fits(se, nb)) return GPU_ACTOR_ERANGE;    // more buckets than a workgroup's LDS holds
+  const size_t dyn = step_dyn_bytes(se, nb);
   // a two-pass table's step as two launches: its two-pass zones, then the rest
   // (zone_dev.h k_step PM)
   const bool split = se.plan && g.split_plan;
@@ -1397,7 +1489,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
       if(rc) return rc;
       g.par ^= 1u;
       g.sidx--;
-      HIPCK(hipMemsetAsync(g.d_pend + slot, 0, sizeof(unsigned long long), g.stream));
+      rc = pend_clear(slot, 1);
+      if(rc) return rc;
       return launch_step(slot, e0, e1);
     }
   }
@@ -1422,6 +1515,10 @@ int launch_pending(uint32_t slot)
 int pend_read(uint32_t first, uint32_t n, std::vector<unsigned long long>& out)
 {
   out.resize(n);
+  {
+    const int rc = fold_counters(first, n);
+    if(rc) return rc;
+  }
   if(R() > 1)
   {
     const int rc = xc_allreduce_sum(g.d_pend + first, g.d_pend + first, n, XC_U64);
@@ -1489,6 +1586,8 @@ void free_all()
   if(g.d_sort_tmp) (void)hipFree(g.d_sort_tmp);
   if(g.d_stats) (void)hipFree(g.d_stats);
   if(g.d_pend) (void)hipFree(g.d_pend);
+  if(g.d_pend_sh) (void)hipFree(g.d_pend_sh);
+  if(g.d_stats_sh) (void)hipFree(g.d_stats_sh);
   if(g.d_dbg) (void)hipFree(g.d_dbg);
   if(g.h_msgs) (void)hipHostFree(g.h_msgs);
   if(g.d_msgs) (void)hipFree(g.d_msgs);
@@ -1616,6 +1715,12 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_stats, ST_COUNT * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats, 0, ST_COUNT * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_pend, kPendSlots * sizeof(unsigned long long)));
+  HIPCK(hipMalloc(&g.d_pend_sh, (size_t)kPendSlots * kShards * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_pend_sh, 0, (size_t)kPendSlots * kShards * sizeof(unsigned long long),
+    g.stream));
+  HIPCK(hipMalloc(&g.d_stats_sh, (size_t)ST_COUNT * kShards * sizeof(unsigned long long)));
+  HIPCK(hipMemsetAsync(g.d_stats_sh, 0, (size_t)ST_COUNT * kShards * sizeof(unsigned long long),
+    g.stream));
   HIPCK(hipMalloc(&g.d_dbg, kMaxZones * kDbgSlots * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_dbg, 0, kMaxZones * kDbgSlots * sizeof(unsigned long long), g.stream));
   HIPCK(hipMalloc(&g.d_spawn_n, sizeof(unsigned int)));
@@ -1754,6 +1859,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   }
   g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
+  g.d_pend_sh = g.d_stats_sh = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
   g.d_spill[0] = g.d_spill[1] = nullptr; g.spill_cap = 0; g.d_sstat = nullptr; g.h_sstat = nullptr;
@@ -1874,7 +1980,7 @@ GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* f
   g.n_actors += count;
   g.n_local = n_local;
   g.n_types = std::max(g.n_types, type_id + 1);
-  int rc = relayout_zones();
+  int rc = relayout_zones(true);
   if(rc) return rc;
   rc = ensure_spill(spill_cap_for_zones());     // empty between calls: nothing to keep
   if(rc) return rc;
@@ -2002,8 +2108,9 @@ int run_sparse(uint64_t max_steps, SparseCtl& out)
 // Pending mail now (all ranks).
 int pending_now(unsigned long long& out)
 {
-  HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
-  int rc = launch_pending(kPendPre);
+  int rc = pend_clear(kPendPre, 1);
+  if(rc) return rc;
+  rc = launch_pending(kPendPre);
   if(rc) return rc;
   std::vector<unsigned long long> pv;
   rc = pend_read(kPendPre, 1, pv);
@@ -2091,7 +2198,8 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       uint32_t k = kChunk;
       if(max_steps) k = (uint32_t)std::min<uint64_t>(k, max_steps - done);
       // pend[j] = pending at the start of step j (k_step), pend[k] = after the chunk
-      HIPCK(hipMemsetAsync(g.d_pend, 0, (k + 1) * sizeof(unsigned long long), g.stream));
+      rc = pend_clear(0, k + 1);
+      if(rc) return rc;
       for(uint32_t j = 0; j < k; ++j)
       {
         par_at[j] = g.par;
@@ -2229,7 +2337,8 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   double ms_total = 0.0;
   while(left)
   {
-    HIPCK(hipMemsetAsync(g.d_pend, 0, kPendSlots * sizeof(unsigned long long), g.stream));
+    rc = pend_clear(0, kPendSlots);
+    if(rc) return rc;
     const uint32_t par0 = g.par, sidx0 = g.sidx;
     HIPCK(hipEventRecord(g.ev[0], g.stream));
     for(uint64_t j = 0; j < left; ++j)
@@ -2350,8 +2459,11 @@ GPU_ACTOR_API int gpu_actor_counts(gpu_actor_counts_t* out)
   }
   if(!out) return GPU_ACTOR_EINVAL;
   unsigned long long st[ST_COUNT];
-  HIPCK(hipMemsetAsync(g.d_pend + kPendPre, 0, sizeof(unsigned long long), g.stream));
-  int rc = launch_pending(kPendPre);
+  int rc = pend_clear(kPendPre, 1);
+  if(rc) return rc;
+  rc = fold_counters(0, 0);
+  if(rc) return rc;
+  rc = launch_pending(kPendPre);
   if(rc) return rc;
   const unsigned long long* src_stats = g.d_stats;
   if(R() > 1)
@@ -2398,9 +2510,17 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
 {
   std::lock_guard<std::mutex> lk(g.mu);
   if(!g.init || !out) return GPU_ACTOR_ESTATE;
-  const uint64_t v[6] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
-                         g.n_zones};
-  for(uint64_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
+  // + the trigger counts by step index mod 3 (zone_dev.h: read this step's,
+  // add to the next's, clear the one after) and the zone geometry
+  unsigned int tn[3] = {0, 0, 0};
+  if(g.d_trig_n)
+  {
+    HIPCK(hipMemcpyAsync(tn, g.d_trig_n, sizeof(tn), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+  }
+  const uint64_t v[10] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+                          g.n_zones, tn[0], tn[1], tn[2], g.zbits};
+  for(uint64_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
   return 0;
 }
 
@@ -2414,6 +2534,68 @@ GPU_ACTOR_API int gpu_actor_debug_stamps(uint64_t* out, uint64_t n)
   HIPCK(hipMemcpyAsync(out, g.d_dbg, n * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
   return 0;
+}
+
+// Diagnostic (not in the public header): the RCCL bodies of the four
+// cross-rank collectives (xc_allreduce_sum for u8/u32/u64, xc_alltoall_u64,
+// xc_allgather_u64) and a grouped ncclSend/ncclRecv — the calls
+// xc_sendrecv makes — run once on a one-rank communicator over this engine's
+// device (ncclCommInitAll: no bootstrap), on device buffers in the engine's
+// stream, exactly as exchange_step calls them. One rank sums to itself, so
+// out[] reads back what went in: out[0..4) the u64 sum, [4..8) u32,
+// [8..16) u8, [16] all-to-all, [17] all-gather, [18..22) the self
+// send/recv's received words; out[22] = the RCCL version. A one-rank engine
+// only (the comm is swapped in for the call); returns GPU_ACTOR_ECOMM with the
+// failing call on stderr if RCCL refuses.
+GPU_ACTOR_API int gpu_actor_debug_rccl_selftest(uint64_t* out, uint64_t n)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init || !out || n < 23) return GPU_ACTOR_EINVAL;
+  if(R() != 1 || g.comm || g.xp_ar || g.xp_a2a) return GPU_ACTOR_ESTATE;
+  ncclComm_t comm = nullptr;
+  int dev = g.device;
+  NCCLCK(ncclCommInitAll(&comm, 1, &dev));
+  g.comm = comm;
+  unsigned long long* d = nullptr;
+  int rc = 0;
+  auto run = [&]() -> int {
+    HIPCK(hipMalloc(&d, 64 * sizeof(unsigned long long)));
+    unsigned long long h[64] = {};
+    for(int i = 0; i < 4; ++i) h[i] = 0x1000000000ull * (i + 1) + i;           // u64
+    uint32_t* h32 = reinterpret_cast<uint32_t*>(h + 4);
+    for(int i = 0; i < 4; ++i) h32[i] = 0x10000u * (i + 1) + 7u;               // u32
+    uint8_t* h8 = reinterpret_cast<uint8_t*>(h + 8);
+    for(int i = 0; i < 64; ++i) h8[i] = (uint8_t)(3 * i + 1);                  // u8
+    h[16] = 0xA2A0000000000001ull;                                               // all-to-all
+    h[17] = 0xA770000000000002ull;                                               // all-gather
+    for(int i = 0; i < 4; ++i) h[24 + i] = 0x5E4D000000000000ull + i;           // send source
+    HIPCK(hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, g.stream));
+    int r = xc_allreduce_sum(d, d, 4, XC_U64);
+    if(!r) r = xc_allreduce_sum(d + 4, d + 4, 8, XC_U32);
+    if(!r) r = xc_allreduce_sum(d + 8, d + 8, 64, XC_U8);
+    if(!r) r = xc_alltoall_u64(d + 16, d + 32);
+    if(!r) r = xc_allgather_u64(d + 17, d + 33);
+    if(r) return r;
+    NCCLCK(ncclGroupStart());
+    NCCLCK(ncclSend(d + 24, 4 * sizeof(unsigned long long), ncclUint8, 0, g.comm, g.stream));
+    NCCLCK(ncclRecv(d + 40, 4 * sizeof(unsigned long long), ncclUint8, 0, g.comm, g.stream));
+    NCCLCK(ncclGroupEnd());
+    HIPCK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    for(int i = 0; i < 16; ++i) out[i] = h[i];
+    out[16] = h[32];
+    out[17] = h[33];
+    for(int i = 0; i < 4; ++i) out[18 + i] = h[40 + i];
+    int ver = 0;
+    NCCLCK(ncclGetVersion(&ver));
+    out[22] = (uint64_t)ver;
+    return 0;
+  };
+  rc = run();
+  if(d) (void)hipFree(d);
+  g.comm = nullptr;
+  (void)ncclCommDestroy(comm);
+  return rc;
 }
 
 } // extern "C"

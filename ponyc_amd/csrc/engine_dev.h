@@ -201,7 +201,16 @@ struct EngDev {
   uint32_t two_pass, pad7;
   // [n_zones] zones the step's two-pass launch ran: step index + 1 (k_step PM 1)
   uint32_t* zplan;
+  // k_step's per-step counters, sharded (pend_sh[slot][kShards],
+  // stats_sh[ST_COUNT][kShards]; zone z adds to shard z % kShards): 512 zones
+  // adding to one word serialise at the memory-side atomic unit (~12 ns each,
+  // MI355X_MICROARCH.md fan-in row), and a zone waits out its own add at its
+  // next barrier. k_fold sums the shards into pend[] / stats[] before the host
+  // reads them.
+  unsigned long long* pend_sh;
+  unsigned long long* stats_sh;
 };
+constexpr uint32_t kShards = 32;
 
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];
@@ -352,15 +361,27 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
         (unsigned long long)arg);
       break;
     case GPU_ACTOR_HT_GUPS_UPDATER: {
+      // t[d & m] ^= d; d == 0 is the identity (send_updater)
       const uint64_t k = arg & (T.params[0] - 1);
-      atomicXor(reinterpret_cast<unsigned long long*>(&T.state[k * T.lcount + li]),
-        (unsigned long long)arg);
+      if(arg != 0)
+        atomicXor(reinterpret_cast<unsigned long long*>(&T.state[k * T.lcount + li]),
+          (unsigned long long)arg);
       break;
     }
     default:
       break;
   }
   (void)beh;
+}
+
+// Per-step counters of zone z (k_step), to its shard
+__device__ __forceinline__ void pend_add_z(uint32_t slot, uint32_t z, unsigned long long v)
+{
+  atomicAdd(&c_eng.pend_sh[(size_t)slot * kShards + (z & (kShards - 1u))], v);
+}
+__device__ __forceinline__ void stat_add_z(int idx, uint32_t z, unsigned long long v)
+{
+  atomicAdd(&c_eng.stats_sh[(size_t)idx * kShards + (z & (kShards - 1u))], v);
 }
 
 // A record whose zone buffer (parity p, landing or carry) is full at `pos`.
@@ -582,10 +603,17 @@ __device__ __forceinline__ void send_updater(A& a, uint32_t to, uint64_t d)
     a.rc_state = T.state;
     a.rc_mask = T.params[0] - 1;
   }
-  // gups_basic Updater.apply: t[d & (size - 1)] ^= d
+  // gups_basic Updater.apply: t[d & (size - 1)] ^= d. An update with d == 0
+  // is the identity and changes no word: it is counted, not issued. (The
+  // reference's PolyRand._seed drops bit 63 of each squaring — its m2 table
+  // has 63 entries — and maps 1/16 of the streamers of C4's wide config to
+  // the seed 0, whose stream stays 0: 65,535 streamers XOR 0 into word 0 of
+  // updater 0 at the same time, one memory-side atomic queue for 1/16 of the
+  // updates; scripts/ubench_gups2.hip, profiles/r05b_ubench_gups2.txt.)
   const uint32_t li = rdiv(to) - a.rc_lfirst;
-  atomicXor(reinterpret_cast<unsigned long long*>(&a.rc_state[(d & a.rc_mask) * a.rc_lcount + li]),
-    (unsigned long long)d);
+  if(d != 0)
+    atomicXor(reinterpret_cast<unsigned long long*>(&a.rc_state[(d & a.rc_mask) * a.rc_lcount + li]),
+      (unsigned long long)d);
 }
 
 // ---- handler tables --------------------------------------------------------

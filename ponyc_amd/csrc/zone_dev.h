@@ -48,6 +48,9 @@ constexpr uint32_t kCarryRun = 256;   // carry records per sample when a backlog
 #ifndef GPA_TILE
 #define GPA_TILE 4096
 #endif
+#ifndef GPA_EMIT_UNROLL
+#define GPA_EMIT_UNROLL 4     // tile records a thread reads before its first store (two-pass emit)
+#endif
 constexpr uint32_t kIdxCap = GPA_IDX_CAP;  // LDS index budget per zone (records per step)
 constexpr uint32_t kTile = GPA_TILE;       // outbox records sorted per scatter tile (64 KB of LDS)
 constexpr int kTilePer = kTile / kZoneThreads;  // tile records per thread
@@ -256,6 +259,35 @@ __device__ __forceinline__ uint4 ld16(const uint4* p)
   uint4 v;
   v.x = p->x; v.y = p->y; v.z = p->z; v.w = p->w;
   return v;
+}
+
+// Stores of a step's output that only the NEXT launch reads (landing records,
+// actor state): with sc1 the line is written through and dropped from the
+// XCD's L2 (MI355X_MICROARCH.md, store flavours), so the launch does not end
+// with up to the L2's capacity of dirty lines to write back at its release
+// (a kernel boundary costs + dirty bytes / ~6 TB/s: the boundary row), and
+// the next launch reads them from another XCD anyway (its acquire invalidates
+// this L2). A vector store (no scalar-cache write).
+#ifndef GPA_STORE_SC1
+#define GPA_STORE_SC1 1
+#endif
+__device__ __forceinline__ void st16_out(uint4* p, const uint4& v)
+{
+#if GPA_STORE_SC1
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v x = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(x) : "memory");
+#else
+  st16(p, v);
+#endif
+}
+__device__ __forceinline__ void st8_out(uint64_t* p, uint64_t v)
+{
+#if GPA_STORE_SC1
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
 }
 
 __device__ __forceinline__ ZRec ld_rec(const ZRec* p)
@@ -975,6 +1007,13 @@ template <int HT> __host__ __device__ constexpr int plan_words()
 }
 constexpr uint32_t kRounds = kZone / kZoneThreads;
 static_assert(kRounds == 4, "two rounds per packed count word, two words");
+constexpr uint32_t kClasses = 16;   // message-count classes of the two-pass dealing (>= 15 share one)
+#ifndef GPA_CLASS_BALLOT
+#define GPA_CLASS_BALLOT 1   // class ranks by ballots (1) or by LDS atomics (0)
+#endif
+#ifndef GPA_PACKED_SCAN
+#define GPA_PACKED_SCAN 1    // pass 2's bucket starts for all rounds in one scan (1) or one per round (0)
+#endif
 // pass 2's tile: the whole LDS pool (the per-actor counts are in registers by then)
 constexpr uint32_t kPlanTile = kTile;
 
@@ -994,12 +1033,47 @@ __device__ __forceinline__ uint32_t emit_rec(const uint4& r, uint32_t b, uint32_
     v.z = r.z;
     v.w = r.w;
     if(pos < zone_capacity(b))
-      st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
+      st16_out(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
     else
       spill_rec(nxt, 0u, b, pos, v);
     return 0;
   }
   return xout_store(b - nz, pos, xpack(r.x, r.y & ~kZoneMask, from, ((uint64_t)r.w << 32) | r.z));
+}
+
+// A chunk's destination word, kept per bucket in LDS for the emit loops: the
+// record offset of its first record in land[nxt] | kDirect when the whole
+// chunk [base, base + h) fits its zone's capacity (the usual case: a record
+// then needs one LDS read for its address, where emit_rec loads the zone's
+// offset and capacity from HBM, a dependent L2 round trip per record), else
+// the reserved position itself (a peer rank's segment, or a chunk that
+// reaches past the zone: emit_rec checks each record).
+constexpr uint32_t kDirect = 0x80000000u;
+__device__ __forceinline__ uint32_t chunk_dst(uint32_t b, uint32_t base, uint32_t h, uint32_t nz)
+{
+  if(b < nz)
+  {
+    const uint64_t o = c_eng.zoff[b] + base;
+    if(base + h <= c_eng.zcapz[b] && o + h <= 0x7FFFFFFFull) return (uint32_t)o | kDirect;
+  }
+  return base;
+}
+
+// Record r of bucket b at offset rel past its chunk's destination word d.
+__device__ __forceinline__ uint32_t emit_at(const uint4& r, uint32_t b, uint32_t d, uint32_t rel,
+  uint32_t L0, uint32_t nz, uint32_t nxt)
+{
+  if(d & kDirect)
+  {
+    uint4 v;
+    v.x = (r.y & ~kZoneMask) | (rdiv(r.x) & kZoneMask);
+    v.y = (L0 + (r.y & kZoneMask)) * c_eng.nranks + c_eng.rank;
+    v.z = r.z;
+    v.w = r.w;
+    st16_out(reinterpret_cast<uint4*>(c_eng.land[nxt] + ((d & ~kDirect) + rel)), v);
+    return 0;
+  }
+  return emit_rec(r, b, d + rel, L0, nz, nxt);
 }
 
 // pass 1: count each send in its (round, bucket) — two rounds per u32 word,
@@ -1017,20 +1091,21 @@ struct PlanCtx : ActorBase {
 // tile holds it at start + rank; past the tile it goes straight to its chunk
 struct TileCtx : ActorBase {
   uint4* tile;
-  uint32_t* cur;          // [nb] bucket cursor in the tile (starts at the bucket's start)
-  const uint32_t* st;     // [nb] bucket start in the tile
-  const uint32_t* bs;     // [nb] next free position of the bucket's chunk
+  uint32_t* cur;          // [nb] bucket cursors in the tile, two rounds per word (half sh)
+  const uint32_t* st;     // [nb] bucket starts in the tile, likewise
+  const uint32_t* bs;     // [nb] the bucket chunk's next free place (chunk_dst word)
+  uint32_t sh, inc;       // this round's half: shift, and 1 << shift
   uint32_t L0, nz, nxt, xover;
   __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg)
   {
     const uint32_t b = bucket_of(to);
-    const uint32_t idx = atomicAdd(&cur[b], 1u);
+    const uint32_t idx = (atomicAdd(&cur[b], inc) >> sh) & 0xFFFFu;
     uint4 r;
     r.x = to; r.y = w | src_local; r.z = (uint32_t)arg; r.w = (uint32_t)(arg >> 32);
     if(idx < kPlanTile)
       tile[idx] = r;
     else
-      xover += emit_rec(r, b, bs[b] + (idx - st[b]), L0, nz, nxt);
+      xover += emit_at(r, b, bs[b], idx - ((st[b] >> sh) & 0xFFFFu), L0, nz, nxt);
   }
 };
 
@@ -1065,7 +1140,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_nout;
   __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
   __shared__ uint32_t s_tot;                // messages pending in the zone (fast path)
-  __shared__ uint32_t s_ph[64];             // two-pass path: actors per message count
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
@@ -1108,8 +1182,16 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     }
     return;
   }
+#ifdef GPA_STAMPS
+  // the device's 100 MHz real-time clock (one for every XCD, unlike the
+  // shader clock of GPA_STAMP): zone start [11] and end [12] across the grid
+  if(tid == 0)
+  {
+    c_eng.dbg[blockIdx.x * kDbgSlots + 11] = __builtin_amdgcn_s_memrealtime();
+    c_eng.dbg[blockIdx.x * kDbgSlots + 12] = 0;
+  }
+#endif
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
-  if(tid < 64) s_ph[tid] = 0;
   if constexpr(kFan)
     for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
   const uint32_t nxt = cur ^ 1u;
@@ -1137,7 +1219,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t ztc = rfl(c_eng.ztrig[cur][z]);
   const uint32_t ztn = rfl(c_eng.ztrig[nxt][z]);
   const bool gate = rfl(c_eng.trig_n[sidx % 3u]) != 0u;
-  if(PM != 1 && z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+  // (every launch of the step clears it — PM 2's zone 0 returns above when PM
+  // 1 ran it; no kernel of this step reads or adds to that slot)
+  if(z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
   if constexpr(PM == 1)
     if(gate || ztc != 0u || (kPlanSplit && c_eng.two_pass == 0u)) return;
   uint8_t* const tb_out = c_eng.trig_own[nxt];
@@ -1283,15 +1367,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
   __syncthreads();
   GPA_STAMP(1);
-  auto take_mail = [&]() __attribute__((always_inline)) {
-    if(tid == 0)
-    {
-      if(nc + nl) atomicAdd(&c_eng.pend[pend_slot], (unsigned long long)(nc + nl));
-      c_eng.carry_n[cur][z] = 0;
-      c_eng.land_n[cur][z] = 0;
-      if constexpr(PM == 1) c_eng.zplan[z] = sidx + 1u;
-    }
-  };
+  // The zone takes its mail: its pending count, the reset of its counters of
+  // parity cur and (PM 1) its mark are stored at the very end of the launch
+  // (nothing in this launch reads them again). Stored here, they were waited
+  // out by the zone's next __syncthreads — a store acknowledgement while the
+  // whole GPU streams its landing buffers.
+  bool took_mail = false;
+  auto take_mail = [&]() __attribute__((always_inline)) { took_mail = true; };
   if constexpr(PM != 1) take_mail();
 
 
@@ -1303,10 +1385,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // then never read — no segment scan, no index, no group sort. Otherwise
   // the zone takes the general path below.
   bool fast = false, plan = false;
-  // two-pass tables: each round's own actor's message count, and its rank
-  // among the zone's actors of the same count class (the plan path deals the
-  // actors to threads by count)
+  // two-pass tables: each round's own actor's message count, its count class
+  // (busiest first) and its rank among its wave's lanes of that class; the
+  // waves' class counts go to s_wcl (the plan path deals the actors to
+  // threads by count). Ranked by ballots: the LDS-atomic ranks they replace
+  // (agg_add, a chain of returning atomics on ~12 hot counters) took 7 % of a
+  // C2 zone (profiles/r05_plan_stamps.txt).
   uint32_t own_n[kRounds], pk[kRounds], prk[kRounds];
+  uint32_t* const s_wcl = s_off;   // [kClasses][kRounds][kZoneWaves]: free until the general path's scan
+#if !GPA_CLASS_BALLOT
+  uint32_t* const s_ph = s_off;    // [kClasses] actors per class (LDS-atomic ranks)
+  for(uint32_t k = tid; k < kClasses; k += kZoneThreads) s_ph[k] = 0;
+  __syncthreads();
+#endif
+  static_assert(kClasses * kRounds * kZoneWaves <= kZone, "class counts fit s_off");
   if constexpr(HTS >= 0 && order_free<HTS>())
     if(!gate && ztc == 0 && tz >= 0)
     {
@@ -1321,15 +1413,32 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         over |= c > bt;
         tot += c;
         if constexpr(two_pass<HTS>())
-        {
-          own_n[r] = i < nact ? c : 0u;
-          pk[r] = 63u - min(own_n[r], 63u);
-          prk[r] = agg_add(s_ph, pk[r], true);
-        }
+          if(PM != 2)
+          {
+            own_n[r] = i < nact ? c : 0u;
+            pk[r] = kClasses - 1u - min(own_n[r], kClasses - 1u);
+#if GPA_CLASS_BALLOT
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            uint32_t rk = 0, wc = 0;
+#pragma unroll
+            for(uint32_t k = 0; k < kClasses; ++k)
+            {
+              const uint64_t m = __ballot(pk[r] == k);
+              if(pk[r] == k) rk = (uint32_t)__popcll(m & lt);
+              if(lane == k) wc = (uint32_t)__popcll(m);
+            }
+            prk[r] = rk;
+            if(lane < kClasses) s_wcl[(lane * kRounds + r) * kZoneWaves + wv] = wc;
+#else
+            prk[r] = agg_add(s_ph, pk[r], true);
+#endif
+          }
       }
+      GPA_STAMP(13);                         // diagnostic build: the class ranks are back
       tot = (uint32_t)min(wave_sum((unsigned long long)tot), 0xFFFFFFFFull);
       if(lane == 0 && tot) atomicAdd(&s_tot, tot);
       fast = !__syncthreads_or(over);
+      GPA_STAMP(14);
       // two passes when every (round, bucket) count fits 16 bits and no
       // actor can run out of sequence numbers (pass 1 would count the
       // overflow again): the zone's messages, each sending at most one, are
@@ -1518,17 +1627,19 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       // ---- 3'. order-free zone: plan, reserve, emit (no outbox) -----------------------
       constexpr int NW = HT_Words<HTS>::W;
       const TypeDev T = c_types[tz];
-      uint32_t* const s_st = s_dyn;             // [nb] bucket totals, then the round's tile starts
-      uint32_t* const s_bs = s_dyn + nb;        // [nb] next free position of each chunk
-      uint32_t* const s_cur = s_dyn + 2 * nb;   // [nb] the round's tile cursors
-      uint32_t* const s_rh = s_dyn + 3 * nb;    // [2][nb] sends per (round, bucket), 16-bit halves
+      // per bucket, two rounds per u32 (16-bit halves: the zone's sends are
+      // fewer than seq_max, so no half carries into the other):
+      uint32_t* const s_rh = s_dyn;             // [2][nb] sends per (round, bucket) -> tile starts
+      uint32_t* const s_cur = s_dyn + 2 * nb;   // [2][nb] tile cursors (from the starts)
+      uint32_t* const s_bs = s_dyn + 4 * nb;    // [2][nb] each chunk's next free place (chunk_dst),
+                                                //   round r reads half r & 1, writes the other
       uint4* const tile = s_pool;                // pass 2 (the whole pool)
       for(uint32_t b = tid; b < 2 * nb; b += kZoneThreads) s_rh[b] = 0;
       // Lanes of a wave run their actors' behaviours side by side, so a wave
       // takes as long as its busiest lane, and the four waves a SIMD holds
       // share its VALU. The zone's actors are therefore dealt to threads by
-      // message count: counting-sorted (busiest first; the class histogram
-      // s_ph was filled beside the fast check) into 64-actor blocks, and
+      // message count: counting-sorted (busiest first; the waves' class counts
+      // s_wcl were written beside the fast check) into 64-actor blocks, and
       // block (wave w, round r) = 8g + (r or 7 - r) for j = w (or W - 1 - w
       // on odd rounds), g = j / 2 — every wave gets alike counts in its lanes
       // and a like total over its rounds, and every round a like share of
@@ -1542,15 +1653,34 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       uint16_t* const s_perm = reinterpret_cast<uint16_t*>(s_pool + kTile) - kZone;
       static_assert(NW * kZone * sizeof(uint64_t) + kZone * sizeof(uint16_t) <= kTile * sizeof(uint4),
                     "two-pass state stage and permutation fit the pool");
+#if GPA_CLASS_BALLOT
+      // (class, round, wave) starts: wave 0 scans the kZone / 4 entries
       if(wv == 0)
       {
-        const uint32_t c = s_ph[lane];
-        s_ph[lane] = wave_incl_scan(c, lane) - c;
+        constexpr uint32_t kE = kClasses * kRounds * kZoneWaves / 64;
+        uint32_t v[kE], sum = 0;
+#pragma unroll
+        for(uint32_t k = 0; k < kE; ++k) { v[k] = s_wcl[lane * kE + k]; sum += v[k]; }
+        uint32_t run = wave_incl_scan(sum, lane) - sum;
+#pragma unroll
+        for(uint32_t k = 0; k < kE; ++k) { s_wcl[lane * kE + k] = run; run += v[k]; }
+      }
+      lds_sync();
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+        s_perm[s_wcl[(pk[r] * kRounds + r) * kZoneWaves + wv] + prk[r]] = (uint16_t)(r * kZoneThreads + tid);
+#else
+      if(wv == 0)
+      {
+        const uint32_t c = lane < kClasses ? s_ph[lane] : 0u;
+        const uint32_t x = wave_incl_scan(c, lane) - c;
+        if(lane < kClasses) s_ph[lane] = x;
       }
       lds_sync();
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
         s_perm[s_ph[pk[r]] + prk[r]] = (uint16_t)(r * kZoneThreads + tid);
+#endif
       lds_sync();
       uint32_t ai[kRounds], nm[kRounds];
 #pragma unroll
@@ -1613,13 +1743,54 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           else
             base = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
         }
-        s_bs[b] = base;
+        s_bs[b] = chunk_dst(b, base, h, nz);
       }
       GPA_STAMP(5);
+#ifdef GPA_STAMPS
+      const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
+#endif
+      // every round's bucket starts in the tile at once: exclusive scans of
+      // the packed (round pair, bucket) counts, in place, each thread a
+      // contiguous run of buckets; the cursors start at them. Three barriers
+      // for the four rounds (a scan per round took three each).
+      uint32_t tot01 = 0, tot23 = 0;
+#if GPA_PACKED_SCAN
+      {
+        const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
+        const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
+        uint32_t a = 0, c = 0;
+        for(uint32_t b = lo; b < hi; ++b) { a += s_rh[b]; c += s_rh[nb + b]; }
+        const uint32_t ia = wave_incl_scan(a, lane), ic = wave_incl_scan(c, lane);
+        if(lane == 63) { s_tmp2[wv] = ia; s_tmp2[kZoneWaves + wv] = ic; }
+        lds_sync();
+        if(wv < 2)
+        {
+          uint32_t* t = s_tmp2 + wv * kZoneWaves;
+          uint32_t x = lane < (uint32_t)kZoneWaves ? t[lane] : 0u;
+          x = wave_incl_scan(x, lane);
+          if(lane < (uint32_t)kZoneWaves) t[lane] = x;
+        }
+        lds_sync();
+        uint32_t ra = (wv ? s_tmp2[wv - 1] : 0u) + ia - a;
+        uint32_t rc = (wv ? s_tmp2[kZoneWaves + wv - 1] : 0u) + ic - c;
+        for(uint32_t b = lo; b < hi; ++b)
+        {
+          const uint32_t va = s_rh[b], vc = s_rh[nb + b];
+          s_rh[b] = ra; s_cur[b] = ra; ra += va;
+          s_rh[nb + b] = rc; s_cur[nb + b] = rc; rc += vc;
+        }
+        tot01 = s_tmp2[kZoneWaves - 1];
+        tot23 = s_tmp2[2 * kZoneWaves - 1];
+        lds_sync();
+      }
+#endif
+#ifdef GPA_STAMPS
+      GPA_ACC(9, t_scan);
+#endif
       // pass 2, one round at a time
       TileCtx tc;
       tc.reset_common();
-      tc.tile = tile; tc.cur = s_cur; tc.st = s_st; tc.bs = s_bs;
+      tc.tile = tile;
       tc.L0 = L0; tc.nz = nz; tc.nxt = nxt; tc.xover = 0;
       uint32_t dz = 0;
 #ifdef GPA_STAMPS
@@ -1628,18 +1799,23 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
       {
-#ifdef GPA_STAMPS
-        const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
-#endif
-        // the round's bucket starts in the tile: an exclusive scan of its
-        // counts, each thread a contiguous run of buckets
+#if GPA_PACKED_SCAN
+        const uint32_t sh = (r & 1u) * 16u;
+        const uint32_t* const rst = s_rh + (r >> 1) * nb;       // the round's starts (half sh)
+        const uint32_t tr = (((r >> 1) ? tot23 : tot01) >> sh) & 0xFFFFu;   // the round's sends
+        tc.cur = s_cur + (r >> 1) * nb;
+#else
+        // the round's own scan (three barriers), into unpacked starts / cursors
+        const uint32_t sh = 0;
+        uint32_t* const rst = s_cur + nb;
+        uint32_t tr;
         {
           const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
           const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
           const uint32_t* rw = s_rh + (r >> 1) * nb;
-          const uint32_t sh = (r & 1u) * 16u;
+          const uint32_t hs = (r & 1u) * 16u;
           uint32_t sum = 0;
-          for(uint32_t b = lo; b < hi; ++b) sum += (rw[b] >> sh) & 0xFFFFu;
+          for(uint32_t b = lo; b < hi; ++b) sum += (rw[b] >> hs) & 0xFFFFu;
           const uint32_t incl = wave_incl_scan(sum, lane);
           if(lane == 63) s_tmp[wv] = incl;
           lds_sync();
@@ -1653,15 +1829,20 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
           for(uint32_t b = lo; b < hi; ++b)
           {
-            s_st[b] = run;
+            rst[b] = run;
             s_cur[b] = run;
-            run += (rw[b] >> sh) & 0xFFFFu;
+            run += (rw[b] >> hs) & 0xFFFFu;
           }
+          tr = s_tmp[kZoneWaves - 1];
+          lds_sync();
         }
-        const uint32_t tr = s_tmp[kZoneWaves - 1];     // the round's sends
-        lds_sync();
+        tc.cur = s_cur;
+#endif
+        const uint32_t* const bsr = s_bs + (r & 1u) * nb;
+        uint32_t* const bsw = s_bs + ((r & 1u) ^ 1u) * nb;
+        tc.st = rst; tc.bs = bsr;
+        tc.sh = sh; tc.inc = 1u << sh;
 #ifdef GPA_STAMPS
-        GPA_ACC(9, t_scan);
         const unsigned long long t_hand = __builtin_amdgcn_s_memtime();
 #endif
         if(nm[r])
@@ -1688,21 +1869,45 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         GPA_ACC(10, t_hand);
         t_emit = __builtin_amdgcn_s_memtime();
 #endif
-        // the tile, sorted by bucket, to the chunks: runs of one chunk per wave store
-        const uint32_t m = min(tr, kPlanTile);
-        for(uint32_t q = tid; q < m; q += kZoneThreads)
+        // the tile, sorted by bucket, to the chunks: runs of one chunk per wave
+        // store; every record of the thread read before the first store
         {
-          const uint4 rec = tile[q];
-          const uint32_t b = bucket_of(rec.x);
-          xover += emit_rec(rec, b, s_bs[b] + (q - s_st[b]), L0, nz, nxt);
+          const uint32_t m = min(tr, kPlanTile);
+          constexpr uint32_t kEU = GPA_EMIT_UNROLL;
+          for(uint32_t q0 = 0; q0 < m; q0 += kEU * kZoneThreads)
+          {
+            uint4 rec[kEU];
+#pragma unroll
+            for(uint32_t u = 0; u < kEU; ++u)
+            {
+              const uint32_t q = q0 + u * kZoneThreads + tid;
+              if(q < m) rec[u] = tile[q];
+            }
+#pragma unroll
+            for(uint32_t u = 0; u < kEU; ++u)
+            {
+              const uint32_t q = q0 + u * kZoneThreads + tid;
+              if(q < m)
+              {
+                const uint32_t b = bucket_of(rec[u].x);
+                xover += emit_at(rec[u], b, bsr[b], q - ((rst[b] >> sh) & 0xFFFFu), L0, nz, nxt);
+              }
+            }
+          }
+        }
+        // the chunks' next free places, for the next round (the other half:
+        // this round's emit still reads this one): + the round's count of the
+        // bucket, the difference of consecutive starts
+        for(uint32_t b = tid; b < nb; b += kZoneThreads)
+        {
+          const uint32_t s0 = (rst[b] >> sh) & 0xFFFFu;
+          const uint32_t s1 = b + 1 < nb ? (rst[b + 1] >> sh) & 0xFFFFu : tr;
+          bsw[b] = bsr[b] + (s1 - s0);
         }
         lds_sync();
 #ifdef GPA_STAMPS
         emit_clk += __builtin_amdgcn_s_memtime() - t_emit;
 #endif
-        // the chunks' next free positions
-        for(uint32_t b = tid; b < nb; b += kZoneThreads)
-          s_bs[b] += (s_rh[(r >> 1) * nb + b] >> ((r & 1u) * 16u)) & 0xFFFFu;
       }
       // the new state back through the stage: permuted into LDS, coalesced out
       // (the last round's emit is behind a barrier: the pool is free)
@@ -1719,7 +1924,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         if(own_n[r])
 #pragma unroll
           for(int k = 0; k < NW; ++k)
-            T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] = s_stage[k * kZone + i];
+            st8_out(&T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)], s_stage[k * kZone + i]);
       }
 #ifdef GPA_STAMPS
       if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 2] = emit_clk;
@@ -1967,7 +2172,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __syncthreads();
   GPA_STAMP(4);
   if(tid < GPU_ACTOR_MAX_TYPES && s_bytype[tid])
-    atomicAdd(&c_eng.stats[ST_BY_TYPE + tid], s_bytype[tid]);
+    stat_add_z(ST_BY_TYPE + tid, z, s_bytype[tid]);
   if constexpr(kFan)
     if(a.fan)
     {
@@ -1992,10 +2197,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     if(h)
     {
       ++n_atom;
-      if(b < nz)
-        s_base[b] = atomicAdd(&c_eng.land_n[nxt][b], h);
-      else
-        s_base[b] = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
+      const uint32_t base = b < nz ? atomicAdd(&c_eng.land_n[nxt][b], h)
+                                   : (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
+      s_base[b] = chunk_dst(b, base, h, nz);
     }
     s_tcnt[b] = 0;
   }
@@ -2007,9 +2211,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // scripts/ubench_scatter.hip).
   const uint32_t nout = min(s_nout, cap);
   const ORec* Oz = c_eng.O + zo;
-  // r = {to, w, arg lo, arg hi} -> position pos of bucket b's chunk
-  auto emit = [&](const uint4& r, uint32_t b, uint32_t pos) __attribute__((always_inline)) {
-    xover += emit_rec(r, b, pos, L0, nz, nxt);
+  // r = {to, w, arg lo, arg hi} -> place rel of bucket b's chunk
+  auto emit = [&](const uint4& r, uint32_t b, uint32_t rel) __attribute__((always_inline)) {
+    xover += emit_at(r, b, s_base[b], rel, L0, nz, nxt);
   };
   if(nout <= kZoneThreads)
   {
@@ -2020,7 +2224,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     {
       const uint4 r = ld16(reinterpret_cast<const uint4*>(Oz + tid));
       const uint32_t b = bucket_of(r.x);
-      emit(r, b, s_base[b] + atomicAdd(&s_tcnt[b], 1u));
+      emit(r, b, atomicAdd(&s_tcnt[b], 1u));
     }
   }
   else
@@ -2062,7 +2266,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     {
       const uint4 r = s_pool[p];
       const uint32_t b = bucket_of(r.x);
-      emit(r, b, s_base[b] + (p - s_tst[b]));
+      emit(r, b, p - s_tst[b]);
     }
     lds_sync();
     for(uint32_t b = tid; b < nb; b += kZoneThreads)
@@ -2090,8 +2294,18 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     for(int w = 0; w < kZoneWaves; ++w) tot += s_red[w][tid];
     const int idx = tid == 0 ? ST_DELIVERED : tid == 1 ? ST_SENT : tid == 2 ? ST_ACTIVE
                   : tid == 3 ? ST_DROPPED : tid == 4 ? ST_XCHG_OVERFLOW : ST_ATOMICS;
-    if(tot) atomicAdd(&c_eng.stats[idx], tot);
+    if(tot) stat_add_z(idx, z, tot);
   }
+  if(took_mail && tid == 0)
+  {
+    if(nc + nl) pend_add_z(pend_slot, z, (unsigned long long)(nc + nl));
+    c_eng.carry_n[cur][z] = 0;
+    c_eng.land_n[cur][z] = 0;
+    if constexpr(PM == 1) c_eng.zplan[z] = sidx + 1u;
+  }
+#ifdef GPA_STAMPS
+  if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 12] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // The helper kernels below belong to engine.hip's code object only (the

@@ -362,12 +362,13 @@ class Engine:
 
     def debug_info(self) -> dict:
         """Engine internals (diagnostic export, not in include/gpu_actor.h)."""
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 10)()
         fn = self.lib.gpu_actor_debug_info
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         fn.restype = ctypes.c_int
-        _ck("gpu_actor_debug_info", fn(out, 6))
-        keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones"]
+        _ck("gpu_actor_debug_info", fn(out, 10))
+        keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones",
+                "trig_n0", "trig_n1", "trig_n2", "zone_bits"]
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
     def stream(self) -> int:

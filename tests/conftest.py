@@ -8,6 +8,18 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
+def pytest_report_header(config):
+    """The library every GPU test loads, by hash, at the top of each log."""
+    import hashlib
+    lib = os.environ.get("PONYC_AMD_LIB", os.path.join(ROOT, "ponyc_amd", "libgpuactor.so"))
+    try:
+        with open(lib, "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        sha = "missing"
+    return f"gpu_actor library: {os.path.relpath(lib, ROOT)} sha256[:16]={sha}"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libgpuactor.so)")
     config.addinivalue_line("markers", "slow: long-running")

@@ -8,6 +8,7 @@ PONYC_AMD_SPLIT_PLAN=0 runs the one-launch kernel (PM 0). Both must equal the
 oracle: steps where every zone takes PM 1, steps where the batch limit, carried
 mail or a hot group send zones to PM 2, and a forward budget whose ramp-down
 mixes the two in one step — at both zone geometries."""
+import numpy as np
 import pytest
 
 from ponyc_amd import workloads as W
@@ -40,3 +41,34 @@ def test_split_launch(engine_factory, oracle, monkeypatch, name, split, bits):
     setup, result = CASES[name]
     g, o = _both(engine_factory, oracle, setup, result)
     _assert_same(g, o)
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_trigger_slots_clear_after_triggers_stop(engine_factory, oracle, monkeypatch, split):
+    """trig_n (zone_dev.h: read step s's slot, add to s+1's, clear s+2's) goes
+    back to 0 once no actor triggers muting — also when zone 0 of the clearing
+    step runs in the split's first launch (PM 1 never cleared it,
+    so a stale count gated every third step onto the general path). 100 extra
+    pings make actor 0 run a full batch in step 0 (overloaded: a trigger, the
+    oracle's trig_count); no actor triggers after that, while the budgeted
+    pings drain over five more steps in which every zone plans."""
+    monkeypatch.setenv("PONYC_AMD_SPLIT_PLAN", split)
+
+    def setup(e):
+        w = W.ubench(e, 4096, 3, 6)
+        W._sendv(e, W._msgs(np.full(100, w["first"], dtype=np.uint64), W.PINGER_PING, 42))
+        return w
+
+    wo = setup(oracle)
+    trace = []
+    while oracle.run(1):
+        trace.append(oracle.trig_count())
+    assert trace[0] > 0 and not any(trace[1:]) and len(trace) >= 5, trace
+    e = engine_factory()
+    we = setup(e)
+    assert e.run() == len(trace)
+    d = e.debug_info()
+    assert (d["trig_n0"], d["trig_n1"], d["trig_n2"]) == (0, 0, 0), d
+    np.testing.assert_array_equal(W.ubench_result(e, we), W.ubench_result(oracle, wo))
+    ce, co = e.counts(), oracle.counts()
+    assert (ce["delivered"], ce["sent"], ce["pending"]) == (co["delivered"], co["sent"], co["pending"])
