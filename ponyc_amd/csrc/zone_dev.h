@@ -261,35 +261,6 @@ __device__ __forceinline__ uint4 ld16(const uint4* p)
   return v;
 }
 
-// Stores of a step's output that only the NEXT launch reads (landing records,
-// actor state): with sc1 the line is written through and dropped from the
-// XCD's L2 (MI355X_MICROARCH.md, store flavours), so the launch does not end
-// with up to the L2's capacity of dirty lines to write back at its release
-// (a kernel boundary costs + dirty bytes / ~6 TB/s: the boundary row), and
-// the next launch reads them from another XCD anyway (its acquire invalidates
-// this L2). A vector store (no scalar-cache write).
-#ifndef GPA_STORE_SC1
-#define GPA_STORE_SC1 1
-#endif
-__device__ __forceinline__ void st16_out(uint4* p, const uint4& v)
-{
-#if GPA_STORE_SC1
-  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  const u4v x = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(x) : "memory");
-#else
-  st16(p, v);
-#endif
-}
-__device__ __forceinline__ void st8_out(uint64_t* p, uint64_t v)
-{
-#if GPA_STORE_SC1
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
-}
-
 __device__ __forceinline__ ZRec ld_rec(const ZRec* p)
 {
   const uint4 v = *reinterpret_cast<const uint4*>(p);
@@ -1008,12 +979,7 @@ template <int HT> __host__ __device__ constexpr int plan_words()
 constexpr uint32_t kRounds = kZone / kZoneThreads;
 static_assert(kRounds == 4, "two rounds per packed count word, two words");
 constexpr uint32_t kClasses = 16;   // message-count classes of the two-pass dealing (>= 15 share one)
-#ifndef GPA_CLASS_BALLOT
-#define GPA_CLASS_BALLOT 1   // class ranks by ballots (1) or by LDS atomics (0)
-#endif
-#ifndef GPA_PACKED_SCAN
-#define GPA_PACKED_SCAN 1    // pass 2's bucket starts for all rounds in one scan (1) or one per round (0)
-#endif
+
 // pass 2's tile: the whole LDS pool (the per-actor counts are in registers by then)
 constexpr uint32_t kPlanTile = kTile;
 
@@ -1033,7 +999,7 @@ __device__ __forceinline__ uint32_t emit_rec(const uint4& r, uint32_t b, uint32_
     v.z = r.z;
     v.w = r.w;
     if(pos < zone_capacity(b))
-      st16_out(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
+      st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + c_eng.zoff[b] + pos), v);
     else
       spill_rec(nxt, 0u, b, pos, v);
     return 0;
@@ -1070,7 +1036,7 @@ __device__ __forceinline__ uint32_t emit_at(const uint4& r, uint32_t b, uint32_t
     v.y = (L0 + (r.y & kZoneMask)) * c_eng.nranks + c_eng.rank;
     v.z = r.z;
     v.w = r.w;
-    st16_out(reinterpret_cast<uint4*>(c_eng.land[nxt] + ((d & ~kDirect) + rel)), v);
+    st16(reinterpret_cast<uint4*>(c_eng.land[nxt] + ((d & ~kDirect) + rel)), v);
     return 0;
   }
   return emit_rec(r, b, d + rel, L0, nz, nxt);
@@ -1140,6 +1106,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_nout;
   __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
   __shared__ uint32_t s_tot;                // messages pending in the zone (fast path)
+  __shared__ uint32_t s_ph[kClasses];       // two-pass path: actors per message-count class
   __shared__ unsigned long long s_agg[kZoneWaves];
   __shared__ unsigned long long s_red[kZoneWaves][6];
   __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
@@ -1192,6 +1159,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   }
 #endif
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
+  if(tid < kClasses) s_ph[tid] = 0;
   if constexpr(kFan)
     for(uint32_t j = tid; j < 2 * kFanLds; j += kZoneThreads) s_fan[j] = 0;
   const uint32_t nxt = cur ^ 1u;
@@ -1386,19 +1354,9 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // the zone takes the general path below.
   bool fast = false, plan = false;
   // two-pass tables: each round's own actor's message count, its count class
-  // (busiest first) and its rank among its wave's lanes of that class; the
-  // waves' class counts go to s_wcl (the plan path deals the actors to
-  // threads by count). Ranked by ballots: the LDS-atomic ranks they replace
-  // (agg_add, a chain of returning atomics on ~12 hot counters) took 7 % of a
-  // C2 zone (profiles/r05_plan_stamps.txt).
+  // (busiest first) and its rank among the zone's actors of that class (the
+  // plan path deals the actors to threads by count; the class histogram s_ph)
   uint32_t own_n[kRounds], pk[kRounds], prk[kRounds];
-  uint32_t* const s_wcl = s_off;   // [kClasses][kRounds][kZoneWaves]: free until the general path's scan
-#if !GPA_CLASS_BALLOT
-  uint32_t* const s_ph = s_off;    // [kClasses] actors per class (LDS-atomic ranks)
-  for(uint32_t k = tid; k < kClasses; k += kZoneThreads) s_ph[k] = 0;
-  __syncthreads();
-#endif
-  static_assert(kClasses * kRounds * kZoneWaves <= kZone, "class counts fit s_off");
   if constexpr(HTS >= 0 && order_free<HTS>())
     if(!gate && ztc == 0 && tz >= 0)
     {
@@ -1417,21 +1375,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           {
             own_n[r] = i < nact ? c : 0u;
             pk[r] = kClasses - 1u - min(own_n[r], kClasses - 1u);
-#if GPA_CLASS_BALLOT
-            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-            uint32_t rk = 0, wc = 0;
-#pragma unroll
-            for(uint32_t k = 0; k < kClasses; ++k)
-            {
-              const uint64_t m = __ballot(pk[r] == k);
-              if(pk[r] == k) rk = (uint32_t)__popcll(m & lt);
-              if(lane == k) wc = (uint32_t)__popcll(m);
-            }
-            prk[r] = rk;
-            if(lane < kClasses) s_wcl[(lane * kRounds + r) * kZoneWaves + wv] = wc;
-#else
             prk[r] = agg_add(s_ph, pk[r], true);
-#endif
           }
       }
       GPA_STAMP(13);                         // diagnostic build: the class ranks are back
@@ -1638,8 +1582,8 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       // Lanes of a wave run their actors' behaviours side by side, so a wave
       // takes as long as its busiest lane, and the four waves a SIMD holds
       // share its VALU. The zone's actors are therefore dealt to threads by
-      // message count: counting-sorted (busiest first; the waves' class counts
-      // s_wcl were written beside the fast check) into 64-actor blocks, and
+      // message count: counting-sorted (busiest first; the class histogram
+      // s_ph was filled beside the fast check) into 64-actor blocks, and
       // block (wave w, round r) = 8g + (r or 7 - r) for j = w (or W - 1 - w
       // on odd rounds), g = j / 2 — every wave gets alike counts in its lanes
       // and a like total over its rounds, and every round a like share of
@@ -1653,23 +1597,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       uint16_t* const s_perm = reinterpret_cast<uint16_t*>(s_pool + kTile) - kZone;
       static_assert(NW * kZone * sizeof(uint64_t) + kZone * sizeof(uint16_t) <= kTile * sizeof(uint4),
                     "two-pass state stage and permutation fit the pool");
-#if GPA_CLASS_BALLOT
-      // (class, round, wave) starts: wave 0 scans the kZone / 4 entries
-      if(wv == 0)
-      {
-        constexpr uint32_t kE = kClasses * kRounds * kZoneWaves / 64;
-        uint32_t v[kE], sum = 0;
-#pragma unroll
-        for(uint32_t k = 0; k < kE; ++k) { v[k] = s_wcl[lane * kE + k]; sum += v[k]; }
-        uint32_t run = wave_incl_scan(sum, lane) - sum;
-#pragma unroll
-        for(uint32_t k = 0; k < kE; ++k) { s_wcl[lane * kE + k] = run; run += v[k]; }
-      }
-      lds_sync();
-#pragma unroll
-      for(uint32_t r = 0; r < kRounds; ++r)
-        s_perm[s_wcl[(pk[r] * kRounds + r) * kZoneWaves + wv] + prk[r]] = (uint16_t)(r * kZoneThreads + tid);
-#else
       if(wv == 0)
       {
         const uint32_t c = lane < kClasses ? s_ph[lane] : 0u;
@@ -1680,7 +1607,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
         s_perm[s_ph[pk[r]] + prk[r]] = (uint16_t)(r * kZoneThreads + tid);
-#endif
       lds_sync();
       uint32_t ai[kRounds], nm[kRounds];
 #pragma unroll
@@ -1753,8 +1679,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       // the packed (round pair, bucket) counts, in place, each thread a
       // contiguous run of buckets; the cursors start at them. Three barriers
       // for the four rounds (a scan per round took three each).
-      uint32_t tot01 = 0, tot23 = 0;
-#if GPA_PACKED_SCAN
+      uint32_t tot01, tot23;
       {
         const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
         const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
@@ -1783,7 +1708,6 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         tot23 = s_tmp2[2 * kZoneWaves - 1];
         lds_sync();
       }
-#endif
 #ifdef GPA_STAMPS
       GPA_ACC(9, t_scan);
 #endif
@@ -1799,45 +1723,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
 #pragma unroll
       for(uint32_t r = 0; r < kRounds; ++r)
       {
-#if GPA_PACKED_SCAN
         const uint32_t sh = (r & 1u) * 16u;
         const uint32_t* const rst = s_rh + (r >> 1) * nb;       // the round's starts (half sh)
         const uint32_t tr = (((r >> 1) ? tot23 : tot01) >> sh) & 0xFFFFu;   // the round's sends
         tc.cur = s_cur + (r >> 1) * nb;
-#else
-        // the round's own scan (three barriers), into unpacked starts / cursors
-        const uint32_t sh = 0;
-        uint32_t* const rst = s_cur + nb;
-        uint32_t tr;
-        {
-          const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
-          const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
-          const uint32_t* rw = s_rh + (r >> 1) * nb;
-          const uint32_t hs = (r & 1u) * 16u;
-          uint32_t sum = 0;
-          for(uint32_t b = lo; b < hi; ++b) sum += (rw[b] >> hs) & 0xFFFFu;
-          const uint32_t incl = wave_incl_scan(sum, lane);
-          if(lane == 63) s_tmp[wv] = incl;
-          lds_sync();
-          if(wv == 0)
-          {
-            uint32_t x = lane < (uint32_t)kZoneWaves ? s_tmp[lane] : 0u;
-            x = wave_incl_scan(x, lane);
-            if(lane < (uint32_t)kZoneWaves) s_tmp[lane] = x;
-          }
-          lds_sync();
-          uint32_t run = (wv ? s_tmp[wv - 1] : 0u) + incl - sum;
-          for(uint32_t b = lo; b < hi; ++b)
-          {
-            rst[b] = run;
-            s_cur[b] = run;
-            run += (rw[b] >> hs) & 0xFFFFu;
-          }
-          tr = s_tmp[kZoneWaves - 1];
-          lds_sync();
-        }
-        tc.cur = s_cur;
-#endif
         const uint32_t* const bsr = s_bs + (r & 1u) * nb;
         uint32_t* const bsw = s_bs + ((r & 1u) ^ 1u) * nb;
         tc.st = rst; tc.bs = bsr;
@@ -1924,7 +1813,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         if(own_n[r])
 #pragma unroll
           for(int k = 0; k < NW; ++k)
-            st8_out(&T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)], s_stage[k * kZone + i]);
+            T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] = s_stage[k * kZone + i];
       }
 #ifdef GPA_STAMPS
       if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 2] = emit_clk;
