@@ -38,6 +38,7 @@ StepEntry step_entry_fanin_sender();
 StepEntry step_entry_gups_streamer();
 StepEntry step_entry_storm();
 StepEntry step_entry_spreader();
+StepEntry step_entry_fifo_pair();
 } // namespace gpa_z12
 
 using namespace gpa;
@@ -453,7 +454,7 @@ const std::vector<StepEntry>& step_entries()
     gpa_z12::step_entry_any(), gpa_z12::step_entry_ring(), gpa_z12::step_entry_pinger(),
     gpa_z12::step_entry_pinger_det(), gpa_z12::step_entry_fanin_sender(),
     gpa_z12::step_entry_gups_streamer(), gpa_z12::step_entry_storm(),
-    gpa_z12::step_entry_spreader()};
+    gpa_z12::step_entry_spreader(), gpa::step_entry_fifo_pair(), gpa_z12::step_entry_fifo_pair()};
   return v;
 }
 
@@ -1271,13 +1272,17 @@ StepEntry step_entry_for(bool z12)
 {
   int only = -1;
   bool mixed = false;
+  uint32_t set = 0;                     // tables of the serial actors, as bits
   for(const HostType& t : g.types)
   {
     if(!t.created || reducible_ht(t.ht)) continue;
     if(only >= 0 && (uint32_t)only != t.ht) mixed = true;
     only = (int)t.ht;
+    set |= 1u << t.ht;
   }
   if(mixed) only = -1;
+  if(set == ((1u << GPU_ACTOR_HT_FIFO_SRC) | (1u << GPU_ACTOR_HT_FIFO_SINK)))
+    return z12 ? gpa_z12::step_entry_fifo_pair() : gpa::step_entry_fifo_pair();
   switch(only)
   {
     case GPU_ACTOR_HT_RING: return z12 ? gpa_z12::step_entry_ring() : gpa::step_entry_ring();

@@ -41,5 +41,6 @@ StepEntry step_entry_fanin_sender();
 StepEntry step_entry_gups_streamer();
 StepEntry step_entry_storm();
 StepEntry step_entry_spreader();
+StepEntry step_entry_fifo_pair();       // FIFO sources + sinks (zone_dev.h kHtFifoPair)
 
 } // namespace gpa

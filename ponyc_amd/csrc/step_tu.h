@@ -23,7 +23,8 @@ template __global__ void k_step<GPA_STEP_HT, 0>(uint32_t, uint32_t, uint32_t);
 // zones spill least without the cold paths (measured: C2-det, the storm)
 template <int HT, int PM> constexpr step_kernel_t split_kernel()
 {
-  if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM))
+  if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM ||
+                           HT == kHtFifoPair))
     return k_step<HT, PM>;
   else return nullptr;
 }

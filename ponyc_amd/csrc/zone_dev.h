@@ -349,6 +349,12 @@ template <int HT> __host__ __device__ constexpr bool order_free()
   return HT == GPU_ACTOR_HT_PINGER;
 }
 
+// A table set compiled as one k_step instantiation: the FIFO probe's source
+// and sink tables (the hot-receiver shape: sources fan in to order-sensitive
+// sinks). Its drain dispatches on the actor's table between these two only,
+// where the any-mix kernel's switch over every table spilled 1,324 VGPRs.
+constexpr int kHtFifoPair = 64;
+
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
   return HT == GPU_ACTOR_HT_FIFO_SINK;
@@ -1873,7 +1879,18 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       AccS acc = acc_s(i);                                                            \
       d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
     }
-    if constexpr(HTS >= 0)
+    if constexpr(HTS == kHtFifoPair)
+    {
+      if(T.ht == GPU_ACTOR_HT_FIFO_SRC)
+      {
+        ZDRAIN(GPU_ACTOR_HT_FIFO_SRC)
+      }
+      else
+      {
+        ZDRAIN(GPU_ACTOR_HT_FIFO_SINK)
+      }
+    }
+    else if constexpr(HTS >= 0)
     {
       ZDRAIN(HTS)
     }
