@@ -26,6 +26,7 @@
 #include "engine_dev.h"
 #include "zone_dev.h"
 #include "sparse_dev.h"
+#include "hot_dev.h"
 #include "step_entry.h"
 
 // the 4096-actor-zone instantiations (step_*_z12.hip)
@@ -206,13 +207,20 @@ __global__ void __launch_bounds__(kBlock) k_spill_place(const SpillRec* s, uint3
 // its chunk touches (binary search over the bases) and walks on from there,
 // so one overloaded receiver's remainder moves at the whole GPU's bandwidth
 // and no workgroup visits copies outside its chunk. With nothing listed the
-// kernel returns at once; otherwise the last workgroup to finish clears the
-// list for the next step.
+// kernel returns at once. The list's counter is kept per step parity (cur):
+// the next step's k_step clears this one (its zone 0, at its start), so no
+// workgroup here signals another (the last-finisher count and fence took
+// ~6 us a step: 512 adds on one word).
 constexpr uint32_t kBigCopyCap = 4096;
 constexpr uint32_t kBigCopyBlocks = 512;
-__global__ void __launch_bounds__(kBlock) k_carry_big()
+__global__ void __launch_bounds__(kBlock) k_carry_big(uint32_t cur)
 {
-  const unsigned long long v = c_eng.bigc_n[0];   // final: k_step ran to completion before
+  // a step that did not run listed nothing (its counter may hold a list of
+  // two steps before, already copied)
+  const bool halt_now = c_eng.nranks == 1 ? (c_eng.spill_n[cur] != 0u || *c_eng.halt != 0u)
+                                          : (*c_eng.spill_flag != 0u);
+  if(halt_now) return;
+  const unsigned long long v = c_eng.bigc_n[cur];  // final: k_step ran to completion before
   const uint32_t n = min((uint32_t)(v >> 32), c_eng.bigc_cap);
   if(n == 0) return;
   // the listed copies' records: the last one's base + its length (bigc_n's
@@ -242,16 +250,6 @@ __global__ void __launch_bounds__(kBlock) k_carry_big()
                       : *reinterpret_cast<const uint4*>(b.p + (b.perm ? (uint32_t)(b.perm[q] & 0xFFFFFull) : q));
         *reinterpret_cast<uint4*>(b.dst + j) = r;
       }
-    }
-  }
-  __syncthreads();
-  if(threadIdx.x == 0)
-  {
-    __threadfence();
-    if(atomicAdd(&c_eng.bigc_n[1], 1ull) == gridDim.x - 1)
-    {
-      atomicExch(&c_eng.bigc_n[0], 0ull);
-      atomicExch(&c_eng.bigc_n[1], 0ull);
     }
   }
 }
@@ -314,6 +312,9 @@ struct Engine {
   unsigned long long* d_pend = nullptr;
   unsigned long long* d_pend_sh = nullptr;    // [kPendSlots][kShards]: k_step's adds
   unsigned long long* d_stats_sh = nullptr;   // [ST_COUNT][kShards]
+  // hot zones (hot_dev.h k_hot): one allocation, carved into EngDev's arrays
+  uint32_t* d_hot = nullptr;
+  bool hot_on = false;
   unsigned long long* d_dbg = nullptr;   // phase stamps of the diagnostic build
   gpu_msg_t* h_msgs = nullptr; uint64_t h_msgs_cap = 0;
   // gpu_actor_send appends here; flushed (one H2D + k_inject) before the
@@ -478,6 +479,8 @@ bool defer_big_wanted()
   return false;
 }
 
+StepEntry pick_step_entry();
+
 int upload_types()
 {
   TypeDev td[GPU_ACTOR_MAX_TYPES];
@@ -510,6 +513,17 @@ int upload_types()
   e.S = g.d_S; e.O = g.d_O;
   e.stats = g.d_stats; e.pend = g.d_pend;
   e.pend_sh = g.d_pend_sh; e.stats_sh = g.d_stats_sh;
+  {
+    uint32_t* h = g.d_hot;
+    e.hot_prep = h; h += kMaxZones;
+    e.hot_slot = h; h += kMaxZones;
+    e.hot_cnt = h; h += kMaxHot * kHotActors;
+    e.hot_aux = h; h += kMaxHot * 3 * kHotActors;
+    e.hot_hist = h; h += kHotBins;
+    e.hot_bcnt = h; h += kHotBins;
+    e.hot_cur = h; h += kHotBins + kHotActors;
+    e.hot_bar = h;
+  }
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
   e.seq_max = R() > 1 ? kXSeqMax : kSeqMax;
   e.dbg = g.d_dbg;
@@ -532,6 +546,13 @@ int upload_types()
   e.xspill = g.d_xspill; e.xspill_n = g.d_xspill_n; e.xspill_cap = g.xspill_cap;
   e.zbits = g.zbits;
   g.defer_big = defer_big_wanted();
+  // k_hot runs where backlogs build (the same engines as defer_big);
+  // PONYC_AMD_HOT=0/1 forces it (tests, A/B)
+  {
+    const char* f = getenv("PONYC_AMD_HOT");
+    g.hot_on = pick_step_entry().hot && (f ? atoi(f) != 0 : g.defer_big);
+    e.hot_on = g.hot_on ? 1u : 0u;
+  }
   e.bigc = g.d_bigc; e.bigc_n = g.d_bigc_n; e.bigc_cap = kBigCopyCap;
   e.defer_big = g.defer_big ? 1u : 0u;
   {
@@ -1456,27 +1477,34 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   // (zone_dev.h k_step PM)
   const bool split = se.plan && g.split_plan;
   step_kernel_t kern = split ? se.plan : se.kernel;
+  // hot zones first (hot_dev.h): the whole GPU prepares them for k_step
+  const size_t hot_lds = 5u * zone_actors() * sizeof(uint32_t);
   if(e0)
   {
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
     const bool more = split || g.defer_big;
+    if(g.hot_on)
+      hipExtLaunchKernelGGL(k_hot, dim3(kHotBlocks), dim3(kHotThreads), (uint32_t)hot_lds, g.stream,
+        e0, nullptr, 0u, g.par, g.sidx);
     hipExtLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
-      e0, more ? nullptr : e1, 0u, g.par, slot, g.sidx);
+      g.hot_on ? nullptr : e0, more ? nullptr : e1, 0u, g.par, slot, g.sidx);
     if(split)
       hipExtLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
         nullptr, g.defer_big ? nullptr : e1, 0u, g.par, slot, g.sidx);
     if(g.defer_big)
       hipExtLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream,
-        nullptr, e1, 0u);
+        nullptr, e1, 0u, g.par);
   }
   else
   {
+    if(g.hot_on)
+      hipLaunchKernelGGL(k_hot, dim3(kHotBlocks), dim3(kHotThreads), hot_lds, g.stream, g.par, g.sidx);
     hipLaunchKernelGGL(kern, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
     if(split)
       hipLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
     if(g.defer_big)
-      hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream);
+      hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream, g.par);
   }
   HIPCK(hipGetLastError());
   const uint32_t step_sidx = g.sidx;
@@ -1593,6 +1621,7 @@ void free_all()
   if(g.d_pend) (void)hipFree(g.d_pend);
   if(g.d_pend_sh) (void)hipFree(g.d_pend_sh);
   if(g.d_stats_sh) (void)hipFree(g.d_stats_sh);
+  if(g.d_hot) (void)hipFree(g.d_hot);
   if(g.d_dbg) (void)hipFree(g.d_dbg);
   if(g.h_msgs) (void)hipHostFree(g.h_msgs);
   if(g.d_msgs) (void)hipFree(g.d_msgs);
@@ -1723,6 +1752,18 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   HIPCK(hipMalloc(&g.d_pend_sh, (size_t)kPendSlots * kShards * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_pend_sh, 0, (size_t)kPendSlots * kShards * sizeof(unsigned long long),
     g.stream));
+  {
+    // hot-zone scratch (hot_dev.h): prep, slot, counts, key ranges (fmin
+    // starts at ~0), bins, bin counts, cursors, barrier
+    const size_t words = 2 * kMaxZones + kMaxHot * kHotActors + kMaxHot * 3 * kHotActors +
+                         3 * (size_t)kHotBins + kHotActors + 64;
+    HIPCK(hipMalloc(&g.d_hot, words * sizeof(uint32_t)));
+    HIPCK(hipMemsetAsync(g.d_hot, 0, words * sizeof(uint32_t), g.stream));
+    uint32_t* aux = g.d_hot + 2 * kMaxZones + kMaxHot * kHotActors;
+    for(uint32_t h = 0; h < kMaxHot; ++h)
+      HIPCK(hipMemsetAsync(aux + (size_t)h * 3 * kHotActors, 0xFF, kHotActors * sizeof(uint32_t),
+        g.stream));
+  }
   HIPCK(hipMalloc(&g.d_stats_sh, (size_t)ST_COUNT * kShards * sizeof(unsigned long long)));
   HIPCK(hipMemsetAsync(g.d_stats_sh, 0, (size_t)ST_COUNT * kShards * sizeof(unsigned long long),
     g.stream));
@@ -1865,6 +1906,7 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.d_S = nullptr; g.d_O = nullptr;
   g.d_stats = g.d_pend = g.d_dbg = nullptr;
   g.d_pend_sh = g.d_stats_sh = nullptr;
+  g.d_hot = nullptr;
   g.spawn_cap = 0; g.d_spawn_n = nullptr; g.d_tstart = g.d_tcnt = nullptr; g.d_live = nullptr;
   g.d_ctl = nullptr; g.h_ctl = nullptr; g.sparse_launches = g.sparse_steps = 0;
   g.d_spill[0] = g.d_spill[1] = nullptr; g.spill_cap = 0; g.d_sstat = nullptr; g.h_sstat = nullptr;

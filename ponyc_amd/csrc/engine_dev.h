@@ -43,7 +43,7 @@ constexpr uint32_t kHostFrom = 0xFF000000u;      // host senders rank above ever
 constexpr uint32_t kSeqMax = 0xFFFEu;            // per-sender sends per step
 constexpr uint32_t kSeqApply = 0xFFFFu;          // outbox marker: reducible apply
 constexpr uint32_t kFanLds = 256;                // analyzers a zone accumulates in LDS
-constexpr uint32_t kDbgSlots = 16;               // diagnostic build: clock stamps per zone
+constexpr uint32_t kDbgSlots = 24;               // diagnostic build: clock stamps per zone
 
 enum Stat : int {
   ST_DELIVERED = 0, ST_SENT = 1, ST_DROPPED = 2, ST_REMOTE_OUT = 3, ST_REMOTE_IN = 4,
@@ -209,6 +209,20 @@ struct EngDev {
   // reads them.
   unsigned long long* pend_sh;
   unsigned long long* stats_sh;
+  // hot zones prepared by the whole GPU before k_step (hot_dev.h k_hot):
+  // hot_prep[z] = step index + 1 of the step whose arrivals k_hot placed in
+  // S, hot_slot[z] its slot; per slot the arrivals per actor (hot_cnt,
+  // [kMaxHot][4096], cleared by k_step as it reads them) and key ranges
+  // (hot_aux); bins and cursors over the zone's big groups; the grid barrier
+  uint32_t hot_on, pad8;
+  uint32_t* hot_prep;
+  uint32_t* hot_slot;
+  uint32_t* hot_cnt;
+  uint32_t* hot_aux;
+  uint32_t* hot_hist;
+  uint32_t* hot_bcnt;
+  uint32_t* hot_cur;
+  uint32_t* hot_bar;
 };
 constexpr uint32_t kShards = 32;
 
@@ -758,8 +772,10 @@ template <class A>
 __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SINK>, const TypeDev& T, A& a,
   uint64_t (&s)[11], uint32_t beh, uint64_t arg)
 {
+  // slot = ((arg >> 32) / ns) % 8, in 32-bit arithmetic (the sender index
+  // is 32 bits; a 64-bit division was most of a hot sink's per-message cost)
   const uint64_t ns = T.params[0] ? T.params[0] : 1;
-  const uint32_t slot = (uint32_t)(((arg >> 32) / ns) % 8);
+  const uint32_t slot = ns > 0xFFFFFFFFull ? 0u : (((uint32_t)(arg >> 32) / (uint32_t)ns) & 7u);
   const uint64_t seq = arg & 0xFFFFFFFFull;
   s[1] += 1;
   s[0] = (s[0] ^ arg) * 0x100000001b3ull;

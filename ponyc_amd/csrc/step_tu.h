@@ -42,10 +42,11 @@ hipError_t step_upload(const void* types, const void* eng, hipStream_t s)
 
 #if GPA_STEP_STUB
 StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork, 4u, nullptr, nullptr }; }
+                                      (uint32_t)kZoneThreads, kSortWork, 4u, false, nullptr, nullptr }; }
 #else
 StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT, 0>, step_upload, false, (uint32_t)kZoneBits,
                                       (uint32_t)kZoneThreads, kSortWork, two_pass<GPA_STEP_HT>() ? 6u : 4u,
+                                      GPA_STEP_HT < 0 || GPA_STEP_HT == kHtFifoPair,
                                       split_kernel<GPA_STEP_HT, 1>(), split_kernel<GPA_STEP_HT, 2>() }; }
 #endif
 

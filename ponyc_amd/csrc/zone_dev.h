@@ -312,8 +312,19 @@ struct AccS {
   // a group the workgroup sorted: its sorted items (key << kPayBits | position
   // in p), read through instead of permuting the records themselves
   const uint64_t* perm = nullptr;
+  // the canonical prefix [0, nst) staged in LDS by the workgroup (k_step:
+  // long sequential runs: a backlog's carried mail, a sorted hot group)
+  const uint4* stg = nullptr;
+  uint32_t nst = 0;
   __device__ __forceinline__ ZRec rec(uint32_t j) const
   {
+    if(j < nst)
+    {
+      const uint4 v = stg[j];
+      ZRec r;
+      r.w0 = v.x; r.from = v.y; r.arg = ((uint64_t)v.w << 32) | v.z;
+      return r;
+    }
     if(j < nc) return ld_rec(c + j);
     return ld_rec(p + (perm ? (uint32_t)(perm[j - nc] & 0xFFFFFull) : j - nc));
   }
@@ -338,6 +349,13 @@ struct AccS {
   }
 };
 
+// Staged runs (k_step 2b): actors whose canonical run this step is at least
+// kStageMin records, at most kMaxStage of them, kStageCap records in all
+// (the LDS index area past the carry starts).
+constexpr uint32_t kStageMin = 32;
+constexpr uint32_t kMaxStage = 64;
+constexpr uint32_t kStageCap = (kIdxCap * sizeof(uint16_t) - kZone * sizeof(uint32_t)) / 16;
+
 // Groups handled whole up to this size keep their keys in registers.
 constexpr uint32_t kMedReg = 16;
 
@@ -354,6 +372,13 @@ template <int HT> __host__ __device__ constexpr bool order_free()
 // sinks). Its drain dispatches on the actor's table between these two only,
 // where the any-mix kernel's switch over every table spilled 1,324 VGPRs.
 constexpr int kHtFifoPair = 64;
+
+// records a lane loads ahead in a sequential drain (drain_zone run_seq):
+// the FIFO tables, whose receivers build backlogs; 1 elsewhere (registers)
+template <int HT> __host__ __device__ constexpr uint32_t seq_batch()
+{
+  return (HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_FIFO_SRC) ? 4u : 1u;
+}
 
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
@@ -420,13 +445,40 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
   uint32_t done = 0;
   bool stop = false, sorted = false;
-  while(done < hc && !stop)
-  {
-    const ZRec r = acc.rec(done);
-    handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
-    ++done;
-    stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
+  // records [j0, j0 + cnt) in order; FIFO tables keep kSeqB loads in flight
+  // (a backlog's carried mail and a sorted group are runs of up to a batch:
+  // one load round trip per record held a hot receiver's lane ~50 us a step)
+#define GPA_RUN_SEQ(J0, CNT)                                                            \
+  if constexpr(seq_batch<HT>() == 1)                                                    \
+  {                                                                                     \
+    for(uint32_t k_ = 0; k_ < (CNT) && !stop; ++k_)                                     \
+    {                                                                                   \
+      const ZRec r_ = acc.rec((J0) + k_);                                               \
+      handle(HtTag<HT>{}, T, a, s, (r_.w0 >> 12) & 0xFu, r_.arg);                       \
+      ++done;                                                                           \
+      stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;                              \
+    }                                                                                   \
+  }                                                                                     \
+  else                                                                                  \
+  {                                                                                     \
+    constexpr uint32_t kSeqB = seq_batch<HT>();                                         \
+    for(uint32_t k0_ = 0; k0_ < (CNT) && !stop; k0_ += kSeqB)                           \
+    {                                                                                   \
+      ZRec r_[kSeqB];                                                                   \
+      _Pragma("unroll")                                                                 \
+      for(uint32_t u_ = 0; u_ < kSeqB; ++u_)                                            \
+        if(k0_ + u_ < (CNT)) r_[u_] = acc.rec((J0) + k0_ + u_);                         \
+      _Pragma("unroll")                                                                 \
+      for(uint32_t u_ = 0; u_ < kSeqB; ++u_)                                            \
+        if(k0_ + u_ < (CNT) && !stop)                                                   \
+        {                                                                               \
+          handle(HtTag<HT>{}, T, a, s, (r_[u_].w0 >> 12) & 0xFu, r_[u_].arg);           \
+          ++done;                                                                       \
+          stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;                          \
+        }                                                                               \
+    }                                                                                   \
   }
+  GPA_RUN_SEQ(0u, hc)
   if(g > 0 && !stop)
   {
     const uint32_t q = w - done;
@@ -534,13 +586,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
       // workgroup already): canonical order first
       if(!presorted) acc.sort(nc, g);
       sorted = true;
-      for(uint32_t k = 0; k < q && !stop; ++k)
-      {
-        const ZRec r = acc.rec(nc + k);
-        handle(HtTag<HT>{}, T, a, s, (r.w0 >> 12) & 0xFu, r.arg);
-        ++done;
-        stop = (a.mute_hit | (kY ? a.yield_req : 0u)) != 0u;
-      }
+      GPA_RUN_SEQ(nc, q)
     }
   }
 #pragma unroll
@@ -550,6 +596,7 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
   if(done < n && g > 1 && !sorted && !presorted) acc.sort(nc, g);
   return done;
 }
+#undef GPA_RUN_SEQ
 
 // The unhandled tail [done, n) of an actor's segment, already canonical, to
 // the next step's carry buffer at carry position co (positions past the
@@ -1122,6 +1169,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   __shared__ uint32_t s_red3[3];
   __shared__ uint32_t s_big[kMaxBig];
   __shared__ uint32_t s_nbig;
+  __shared__ uint32_t s_stn, s_stl[kMaxStage], s_stc[kMaxStage], s_sto[kMaxStage + 1];   // staged runs
   constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
   __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
@@ -1194,8 +1242,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t ztn = rfl(c_eng.ztrig[nxt][z]);
   const bool gate = rfl(c_eng.trig_n[sidx % 3u]) != 0u;
   // (every launch of the step clears it — PM 2's zone 0 returns above when PM
-  // 1 ran it; no kernel of this step reads or adds to that slot)
-  if(z == 0 && tid == 0) c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+  // 1 ran it; no kernel of this step reads or adds to that slot). Likewise the
+  // backlog list of the other parity, which the last k_carry_big copied.
+  if(z == 0 && tid == 0)
+  {
+    c_eng.trig_n[(sidx + 2u) % 3u] = 0u;
+    c_eng.bigc_n[cur ^ 1u] = 0ull;
+  }
   if constexpr(PM == 1)
     if(gate || ztc != 0u || (kPlanSplit && c_eng.two_pass == 0u)) return;
   uint8_t* const tb_out = c_eng.trig_own[nxt];
@@ -1235,6 +1288,14 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const ZRec* C = c_eng.carry[cur] + zo;
   const ZRec* Ld = c_eng.land[cur] + zo;
   const bool use_idx = kSimple || nc + nl <= kIdxCap;       // uniform per workgroup
+  // a hot zone k_hot prepared: its arrivals are in S already, counted in
+  // hot_cnt, each big group sorted (hot_dev.h)
+  // (compiled for the tables whose engines run k_hot: engine.hip hot_on)
+  constexpr bool kHotTables = !kSimple && (HTS < 0 || HTS == kHtFifoPair);
+  const bool hot = kHotTables && c_eng.hot_on &&
+                   __builtin_amdgcn_readfirstlane(c_eng.hot_prep[z]) == sidx + 1u;
+  const uint32_t* const hot_cnt =
+    c_eng.hot_cnt + (size_t)__builtin_amdgcn_readfirstlane(hot ? c_eng.hot_slot[z] : 0u) * 4096u;
   // carried records counted apart (s_ccnt); landed ones in s_cnt.
   // Carried mail is sorted by actor (carry-out writes each actor's remainder
   // at its scan offset). A large carry (a backlog) is counted from samples:
@@ -1324,6 +1385,12 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         wr[u] = (atomicAdd(&s_cnt[act], 1u) << kZoneBits) | act;
       }
   }
+  else if(hot)
+    for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+    {
+      s_cnt[i] = hot_cnt[i];
+      const_cast<uint32_t*>(hot_cnt)[i] = 0;     // (k_hot's next use of the slot is a later launch)
+    }
   else
   for(uint32_t base = 0; base < nl; base += kZoneThreads * kUnroll)
   {
@@ -1500,7 +1567,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       for(int u = 0; u < kH; ++u)
         if(r[u].x != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(Sz + pos[u]) = r[u];
     };
-    if(nl)
+    if(nl && !hot)
     {
       uint4 ra[kH], rb[kH];
       load_half(ra, 0);
@@ -1527,8 +1594,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   for(uint32_t i = tid; i < nact; i += kZoneThreads)
     if(s_cnt[i] - s_ccnt[i] > kBigGroup)
     {
-      const uint32_t k = atomicAdd(&s_nbig, 1u);
-      if(k < kMaxBig) s_big[k] = i;
+      if(hot)
+        atomicOr(&s_bigbits[i >> 5], 1u << (i & 31));   // sorted by k_hot, in place
+      else
+      {
+        const uint32_t k = atomicAdd(&s_nbig, 1u);
+        if(k < kMaxBig) s_big[k] = i;
+      }
     }
   __syncthreads();
   {
@@ -1561,7 +1633,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // S path accessor of actor i (a group the workgroup sorted: read through its items)
   auto acc_s = [&](uint32_t i) __attribute__((always_inline)) {
     AccS a_{Sz + s_off[i], C + s_cst[i], s_ccnt[i]};
-    if(big_sorted(i)) a_.perm = perm_s + s_off[i];
+    if(big_sorted(i) && !hot) a_.perm = perm_s + s_off[i];
     return a_;
   };
 
@@ -1834,6 +1906,63 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
   int any_rem = 0;
 
+  // ---- 2b. staged runs (scratch path): an actor that handles a long run of
+  // records in canonical order — its carried mail, then its arrivals when the
+  // workgroup or k_hot sorted them — reads them one after another, a memory
+  // round trip each (a hot receiver's backlog: 100 a step, ~40 us of its
+  // zone). The workgroup loads the prefix each such actor handles this step
+  // into LDS first (the index area past the carry starts, free on this path),
+  // all loads in flight; s_aux[i] = stage offset << 16 | records until the
+  // actor's own drain overwrites it.
+  bool staged = false;
+  uint4* const s_stage = reinterpret_cast<uint4*>(s_cst + kZone);
+  if constexpr(!kSimple)
+    if(!use_idx && !fast)
+    {
+      if(tid == 0) s_stn = 0;
+      __syncthreads();
+      for(uint32_t i = tid; i < nact; i += kZoneThreads)
+      {
+        const uint32_t n = s_cnt[i];
+        if(n < kStageMin) continue;
+        const int t = tz >= 0 ? tz : type_of_local(L0 + i);
+        if(t < 0 || c_types[t].reducible) continue;
+        const uint32_t w = c_types[t].prio ? n : min(n, c_types[t].batch);
+        const uint32_t run = min(w, big_sorted(i) ? n : s_ccnt[i]);   // the canonical prefix handled
+        if(run < kStageMin) continue;
+        const uint32_t k = atomicAdd(&s_stn, 1u);
+        if(k < kMaxStage) { s_stl[k] = i; s_stc[k] = run; }
+      }
+      __syncthreads();
+      const uint32_t ns = min(s_stn, kMaxStage);
+      if(ns)
+      {
+        if(tid == 0)
+        {
+          uint32_t o = 0;
+          for(uint32_t k = 0; k < ns; ++k)
+          {
+            const uint32_t c = min(s_stc[k], kStageCap - o);
+            s_sto[k] = o; s_stc[k] = c; o += c;
+          }
+          s_sto[ns] = o;
+        }
+        __syncthreads();
+        if(tid < ns && s_stc[tid]) s_aux[s_stl[tid]] = (s_sto[tid] << 16) | s_stc[tid];
+        const uint32_t tot = s_sto[ns];
+        for(uint32_t t0 = tid; t0 < tot; t0 += kZoneThreads)
+        {
+          uint32_t k = 0;
+          while(k + 1 < ns && s_sto[k + 1] <= t0) ++k;
+          const ZRec r = acc_s(s_stl[k]).rec(t0 - s_sto[k]);
+          s_stage[t0] = make_uint4(r.w0, r.from, (uint32_t)r.arg, (uint32_t)(r.arg >> 32));
+        }
+        __syncthreads();
+        staged = true;
+      }
+    }
+  GPA_STAMP(15);                         // diagnostic build: staged runs loaded
+
   // ---- 3. run handlers -------------------------------------------------------------
   a.out = c_eng.O + zo;
   a.s_nout = &s_nout;
@@ -1877,6 +2006,11 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     else                                                                              \
     {                                                                                 \
       AccS acc = acc_s(i);                                                            \
+      if(staged)                                                                      \
+      {                                                                               \
+        const uint32_t sg = s_aux[i];                                                 \
+        if(sg) { acc.stg = s_stage + (sg >> 16); acc.nst = sg & 0xFFFFu; }            \
+      }                                                                               \
       d = zone_actor<HT>(T, a, acc, n, s_ccnt[i], stays, big_sorted(i));              \
     }
     if constexpr(HTS == kHtFifoPair)
@@ -1949,6 +2083,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       if(d) atomicAdd(&s_bytype[t], (unsigned long long)d);
     }
   }
+  GPA_STAMP(16);                         // diagnostic build: the drain ends
   sent = a.sent;
   applied = a.applied;
   if(applied && a.applied_type >= 0)
@@ -1994,7 +2129,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
         if(tid == 0)
         {
           // one atomic gives the slot and the copy's place in the flat list
-          const unsigned long long v = atomicAdd(&c_eng.bigc_n[0], (1ull << 32) | rem);
+          const unsigned long long v = atomicAdd(&c_eng.bigc_n[cur], (1ull << 32) | rem);
           const uint32_t slot = (uint32_t)(v >> 32);
           uint32_t ok = 0;
           if(slot < c_eng.bigc_cap)
@@ -2002,7 +2137,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
             BigCopy b;
             b.c = C + s_cst[i]; b.p = Sz + s_off[i]; b.dst = cout + co;
             b.ncc = s_ccnt[i]; b.from = n - rem; b.rem = rem; b.base = (uint32_t)v;
-            b.perm = big_sorted(i) ? perm_s + s_off[i] : nullptr;
+            b.perm = big_sorted(i) && !hot ? perm_s + s_off[i] : nullptr;
             c_eng.bigc[slot] = b;
             ok = 1;
           }

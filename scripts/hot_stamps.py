@@ -24,12 +24,16 @@ lib.gpu_actor_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nz = (100_004 + 2047) // 2048
 for step in range(4):
     e.run_fixed(1)
-    buf = np.zeros(nz * 16, dtype=np.uint64)
+    buf = np.zeros(nz * 24, dtype=np.uint64)
     lib.gpu_actor_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-    st = buf.reshape(nz, 16).astype(np.int64)[0]
+    st = buf.reshape(nz, 24).astype(np.int64)[0]
     order = [(0, 1, "count"), (1, 2, "scans"), (2, 3, "place"), (3, 7, "big sort"),
-             (7, 4, "behaviours+carry"), (4, 5, "reserve"), (5, 6, "scatter")]
+             (7, 15, "stage"), (15, 16, "behaviours"), (16, 4, "carry-out"), (4, 5, "reserve"), (5, 6, "scatter")]
     parts = {nm: int(st[b] - st[a]) for a, b, nm in order}
-    print(f"step {step}: step_us={e.last_drain_ms() * 1e3:.1f} zone0 span={int(st[6] - st[0])} clk",
-          parts)
+    allz = buf.reshape(nz, 24).astype(np.int64)
+    ok = allz[:, 12] >= allz[:, 11]
+    t0 = allz[ok, 11].min()
+    print(f"step {step}: step_us={e.last_drain_ms() * 1e3:.1f} zone0 span={int(st[6] - st[0])} clk "
+          f"real {0.01 * (st[12] - st[11]):.1f} us (start +{0.01 * (st[11] - t0):.1f}); "
+          f"other zones end by {0.01 * (allz[ok, 12].max() - t0):.1f} us", parts)
 e.shutdown()

@@ -17,7 +17,7 @@ for f in files:
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
 rows.sort()
-ks = [r for r in rows if "k_step" in r[2] or "k_carry_big" in r[2]]
+ks = [r for r in rows if any(k in r[2] for k in ("k_step", "k_carry_big", "k_hot", "k_sparse"))]
 def short(n):
     return n.split("(")[0].replace("void ", "")
 kinds = {}

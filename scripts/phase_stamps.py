@@ -34,9 +34,9 @@ lib = eng.lib
 lib.gpu_actor_debug_stamps.restype = ctypes.c_int
 lib.gpu_actor_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nz = (N + 2047) // 2048
-buf = np.zeros(nz * 16, dtype=np.uint64)
+buf = np.zeros(nz * 24, dtype=np.uint64)
 lib.gpu_actor_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-st = buf.reshape(nz, 16).astype(np.int64)
+st = buf.reshape(nz, 24).astype(np.int64)
 names = ["count", "scans", "place S", "handlers", "reserve", "scatter"]
 d = np.diff(st[:, :7], axis=1)
 tot = st[:, 6] - st[:, 0]

@@ -33,9 +33,9 @@ lib = eng.lib
 lib.gpu_actor_debug_stamps.restype = ctypes.c_int
 lib.gpu_actor_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nz = eng.debug_info()["zones"]
-buf = np.zeros(nz * 16, dtype=np.uint64)
+buf = np.zeros(nz * 24, dtype=np.uint64)
 lib.gpu_actor_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size)
-st = buf.reshape(nz, 16).astype(np.int64)
+st = buf.reshape(nz, 24).astype(np.int64)
 tot = st[:, 6] - st[:, 0]
 parts = [("count", st[:, 1] - st[:, 0]), ("fast check", st[:, 7] - st[:, 1]),
          ("  class ranks", st[:, 13] - st[:, 1]), ("  fast vote", st[:, 14] - st[:, 13]),

@@ -114,14 +114,19 @@ def test_backlog_copies(engine_factory, oracle, monkeypatch, defer, sources, sin
           W.fifo_result, mailbox_cap=16)
 
 
+@pytest.mark.parametrize("hot", ["0", "1"])
 @pytest.mark.parametrize("m", [5, 20, 40])
-def test_hot_group_sort_paths(engine_factory, oracle, m):
+def test_hot_group_sort_paths(engine_factory, oracle, monkeypatch, m, hot):
     """A hot sink's arrival group sorted by the workgroup (zone_dev.h
     coop_msd_sort): 3000 sources burst m PUSHes each at one sink. The MSD
     pass bins the keys by their top 11 bits — the sender id's high bits — so
     each bin holds 2m items: m=5 sorts its bins in registers (15,000 arrivals:
     the LDS-index path), m=20 in memory (over 16 items; the scratch path, read
     through the sorted items), m=40 takes the LSD sort (bins over 64; the zone
-    also grows 4x in the burst)."""
+    also grows 4x in the burst). With PONYC_AMD_HOT=1 the zones of 60,000 and
+    120,000 arrivals are prepared by k_hot (hot_dev.h: every CU counts,
+    places and bin-sorts them; bins of one sender's 20 or 40 records sorted
+    in memory) and k_step reads them in place."""
+    monkeypatch.setenv("PONYC_AMD_HOT", hot)
     _both(engine_factory, oracle, lambda e: W.fifo(e, 3000, 1, 1, m, mailbox_cap=16),
           W.fifo_result)
