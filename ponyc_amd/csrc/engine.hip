@@ -383,6 +383,9 @@ struct Engine {
   // two-pass table's step as the two launches (PONYC_AMD_SPLIT_PLAN=0: one)
   uint32_t* d_zplan = nullptr;
   bool split_plan = true;
+  // split tables: the step as one launch (k_step PM 3: the rest through a
+  // call) instead of two (PONYC_AMD_FUSE=0: two)
+  bool fuse = true;
   uint32_t sidx = 0;
   // backlog copies handed to k_carry_big (EngDev::bigc)
   BigCopy* d_bigc = nullptr;
@@ -560,6 +563,8 @@ int upload_types()
     e.two_pass = (f && atoi(f) == 0) ? 0u : 1u;
     const char* sp = getenv("PONYC_AMD_SPLIT_PLAN");
     g.split_plan = !(sp && atoi(sp) == 0);
+    const char* fu = getenv("PONYC_AMD_FUSE");
+    g.fuse = !(fu && atoi(fu) == 0);
   }
   e.zplan = g.d_zplan;
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
@@ -1340,7 +1345,7 @@ bool step_fits(const StepEntry& se, uint64_t nb)
 {
   static std::map<step_kernel_t, size_t> cache;     // (callers hold g.mu)
   size_t st = 0;
-  for(step_kernel_t k : {se.kernel, se.plan, se.rest})
+  for(step_kernel_t k : {se.kernel, se.plan, se.rest, se.fused})
   {
     if(!k) continue;
     auto it = cache.find(k);
@@ -1475,8 +1480,10 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   const size_t dyn = step_dyn_bytes(se, nb);
   // a two-pass table's step as two launches: its two-pass zones, then the rest
   // (zone_dev.h k_step PM)
-  const bool split = se.plan && g.split_plan;
-  step_kernel_t kern = split ? se.plan : se.kernel;
+  // (fused: one launch of PM 3 in their place)
+  const bool fused = se.plan && g.split_plan && g.fuse && se.fused;
+  const bool split = se.plan && g.split_plan && !fused;
+  step_kernel_t kern = fused ? se.fused : split ? se.plan : se.kernel;
   // hot zones first (hot_dev.h): the whole GPU prepares them for k_step
   const size_t hot_lds = 5u * zone_actors() * sizeof(uint32_t);
   if(e0)

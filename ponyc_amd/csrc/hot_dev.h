@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
 {
   extern __shared__ uint32_t s_h[];            // [5][za]
   __shared__ uint32_t s_list[kMaxHot];
-  __shared__ uint32_t s_nlist, s_tot, s_bins;
+  __shared__ uint32_t s_nlist, s_bins;
   __shared__ uint32_t s_tmp[kHotThreads / 64 + 1];
   __shared__ uint32_t s_tmp2[kHotThreads / 64 + 1];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
           const uint32_t tn = s_tmp[w], tb = s_tmp2[w];
           s_tmp[w] = rn; s_tmp2[w] = rb; rn += tn; rb += tb;
         }
-        s_tot = rn; s_bins = rb;
+        s_bins = rb;
       }
       __syncthreads();
       uint32_t rn = s_tmp[wv] + pn - sn, rb = s_tmp2[wv] + pb - sb;

@@ -27,9 +27,9 @@ struct StepEntry {
   uint32_t sort_work;      // u32 of dynamic LDS the hot-group sort borrows
   uint32_t bucket_words;   // u32 of dynamic LDS per destination bucket (6: a two-pass table)
   bool hot;                // takes zones prepared by k_hot (hot_dev.h): any-mix and FIFO pair
-  // two-pass tables: the step as two launches (zone_dev.h k_step PM 1, 2);
-  // nullptr for the other tables
-  step_kernel_t plan, rest;
+  // split tables: the step as two launches (zone_dev.h k_step PM 1, 2), or
+  // as one that calls the second's code (PM 3); nullptr for the other tables
+  step_kernel_t plan, rest, fused;
 };
 
 namespace gpa {

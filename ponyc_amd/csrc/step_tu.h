@@ -21,10 +21,15 @@ template __global__ void k_step_stub<GPA_STEP_HT>(uint32_t, uint32_t, uint32_t);
 template __global__ void k_step<GPA_STEP_HT, 0>(uint32_t, uint32_t, uint32_t);
 // split for the two-pass table and for the general-path tables whose plain
 // zones spill least without the cold paths (measured: C2-det, the storm)
+// PM 3 (one launch, the rest through a call) for the two-pass table only:
+// C2 70.4-71.0 us against 72.3-72.7 as two launches; C2-det 177-178 against
+// 175.6 (profiles/r05w_fused_ab.txt)
 template <int HT, int PM> constexpr step_kernel_t split_kernel()
 {
-  if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM ||
-                           HT == kHtFifoPair))
+  if constexpr(PM == 3 && !(HT >= 0 && two_pass<HT>()))
+    return nullptr;
+  else if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM ||
+                                HT == kHtFifoPair))
     return k_step<HT, PM>;
   else return nullptr;
 }
@@ -42,12 +47,13 @@ hipError_t step_upload(const void* types, const void* eng, hipStream_t s)
 
 #if GPA_STEP_STUB
 StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, true, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork, 4u, false, nullptr, nullptr }; }
+                                      (uint32_t)kZoneThreads, kSortWork, 4u, false, nullptr, nullptr, nullptr }; }
 #else
 StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT, 0>, step_upload, false, (uint32_t)kZoneBits,
                                       (uint32_t)kZoneThreads, kSortWork, two_pass<GPA_STEP_HT>() ? 6u : 4u,
                                       GPA_STEP_HT < 0 || GPA_STEP_HT == kHtFifoPair,
-                                      split_kernel<GPA_STEP_HT, 1>(), split_kernel<GPA_STEP_HT, 2>() }; }
+                                      split_kernel<GPA_STEP_HT, 1>(), split_kernel<GPA_STEP_HT, 2>(),
+                                      split_kernel<GPA_STEP_HT, 3>() }; }
 #endif
 
 } // namespace gpa

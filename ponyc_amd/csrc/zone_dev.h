@@ -32,10 +32,10 @@ namespace gpa {
 // build compiles these away.
 #ifdef GPA_STAMPS
 #define GPA_STAMP(k)                                                         \
-  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * kDbgSlots + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
+  do { if(threadIdx.x == 0) c_eng.dbg[z * kDbgSlots + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
 // diagnostic build: add the clocks since t0 to slot k (thread 0)
 #define GPA_ACC(k, t0)                                                        \
-  do { if(threadIdx.x == 0) c_eng.dbg[blockIdx.x * kDbgSlots + (k)] += __builtin_amdgcn_s_memtime() - (t0); } while(0)
+  do { if(threadIdx.x == 0) c_eng.dbg[z * kDbgSlots + (k)] += __builtin_amdgcn_s_memtime() - (t0); } while(0)
 #else
 #define GPA_STAMP(k) do {} while(0)
 #endif
@@ -1138,13 +1138,51 @@ struct TileCtx : ActorBase {
 // other zone returns before it has written anything — and marks them in
 // c_eng.zplan; PM 2, launched right behind it, runs the rest (the general
 // path, as PM 0 would).
-template <int HTS, int PM>
-__global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
-  uint32_t sidx)
-{
+// A zone's static LDS, one object per table (HTS) whatever the launch form
+// (PM): the fused step (PM 3) runs PM 1's and PM 2's code in one kernel, and
+// function-local __shared__ arrays in the two instantiations would be two
+// allocations.
+template <int HTS> struct ZoneLds {
   // 64 KB pool. Phases 1-3: per-actor arrays + the segment index; phase 4:
   // the outbox sort tile (kTile records).
-  __shared__ uint4 s_pool[kTile];
+  uint4 pool[kTile];
+  uint32_t tmp[kZoneWaves + 1];
+  uint32_t tmp2[2 * kZoneWaves];
+  uint32_t nout;
+  uint32_t nmix;                    // carry runs that straddle actors (count phase)
+  uint32_t tot;                     // messages pending in the zone (fast path)
+  uint32_t ph[kClasses];            // two-pass path: actors per message-count class
+  unsigned long long agg[kZoneWaves];
+  unsigned long long bytype[GPU_ACTOR_MAX_TYPES];
+  __attribute__((aligned(16))) uint8_t tb[kZone];   // trigger byte per actor
+  uint32_t ntrig;
+  uint32_t bigbits[kZone / 32];     // groups the workgroup sorted this step
+  uint32_t red3[3];
+  uint32_t big[kMaxBig];
+  uint32_t nbig;
+  uint32_t stn;
+  // the staged runs' lists (phase 2b) and, once they are spent, the counters'
+  // reduction (the end): apart, the pinger's zone held 160 B more than lets
+  // two workgroups share a CU beside its 12 KB of bucket arrays
+  union {
+    struct { uint32_t stl[kMaxStage], stc[kMaxStage], sto[kMaxStage + 1]; } st;   // staged runs
+    unsigned long long red[kZoneWaves][6];
+  } u;
+  unsigned long long fan[(HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER) ? 2 * kFanLds : 1];   // fan-in apply accumulators
+};
+template <int HTS> __device__ __forceinline__ ZoneLds<HTS>& zone_lds()
+{
+  __shared__ ZoneLds<HTS> lds;
+  return lds;
+}
+
+// zone_step runs zone z's step; k_step (below) maps workgroups to zones.
+template <int HTS, int PM>
+__device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32_t pend_slot,
+  uint32_t sidx)
+{
+  ZoneLds<HTS>& Z = zone_lds<HTS>();
+  uint4* const s_pool = Z.pool;
   static_assert(4 * kZone * sizeof(uint32_t) + kIdxCap * sizeof(uint16_t) <= sizeof(uint4) * kTile,
                 "LDS pool too small");
   uint32_t* const s_cnt = reinterpret_cast<uint32_t*>(s_pool);   // records per actor this step
@@ -1154,26 +1192,29 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   uint16_t* const s_idx = reinterpret_cast<uint16_t*>(s_aux + kZone);  // index into carry ++ landing
   uint32_t* const s_cst = reinterpret_cast<uint32_t*>(s_idx);   // S path: carry start per actor
   extern __shared__ uint32_t s_dyn[];   // [nb] histogram, [nb] chunk bases, [nb] tile counts, [nb] tile starts
-  __shared__ uint32_t s_tmp[kZoneWaves + 1];
-  __shared__ uint32_t s_tmp2[2 * kZoneWaves];
-  __shared__ uint32_t s_nout;
-  __shared__ uint32_t s_nmix;               // carry runs that straddle actors (count phase)
-  __shared__ uint32_t s_tot;                // messages pending in the zone (fast path)
-  __shared__ uint32_t s_ph[kClasses];       // two-pass path: actors per message-count class
-  __shared__ unsigned long long s_agg[kZoneWaves];
-  __shared__ unsigned long long s_red[kZoneWaves][6];
-  __shared__ unsigned long long s_bytype[GPU_ACTOR_MAX_TYPES];
-  __shared__ __attribute__((aligned(16))) uint8_t s_tb[kZone];   // trigger byte per actor
-  __shared__ uint32_t s_ntrig;
-  __shared__ uint32_t s_bigbits[kZone / 32];   // groups the workgroup sorted this step
-  __shared__ uint32_t s_red3[3];
-  __shared__ uint32_t s_big[kMaxBig];
-  __shared__ uint32_t s_nbig;
-  __shared__ uint32_t s_stn, s_stl[kMaxStage], s_stc[kMaxStage], s_sto[kMaxStage + 1];   // staged runs
+  auto& s_tmp = Z.tmp;
+  auto& s_tmp2 = Z.tmp2;
+  auto& s_nout = Z.nout;
+  auto& s_nmix = Z.nmix;
+  auto& s_tot = Z.tot;
+  auto& s_ph = Z.ph;
+  auto& s_agg = Z.agg;
+  auto& s_red = Z.u.red;
+  auto& s_bytype = Z.bytype;
+  auto& s_tb = Z.tb;
+  auto& s_ntrig = Z.ntrig;
+  auto& s_bigbits = Z.bigbits;
+  auto& s_red3 = Z.red3;
+  auto& s_big = Z.big;
+  auto& s_nbig = Z.nbig;
+  auto& s_stn = Z.stn;
+  auto& s_stl = Z.u.st.stl;
+  auto& s_stc = Z.u.st.stc;
+  auto& s_sto = Z.u.st.sto;
+  auto& s_fan = Z.fan;
   constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
-  __shared__ unsigned long long s_fan[kFan ? 2 * kFanLds : 1];   // fan-in apply accumulators
 
-  const uint32_t z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   static_assert(PM == 0 || HTS >= 0, "split launches are for one-table engines");
   // PM 1 of a two-pass table takes the zones that plan; of any other table
   // the plain zones (kSimple): no backpressure, no carried mail, the LDS
@@ -1184,7 +1225,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   // (the mark is the step's index + 1: nothing clears it, and a step that
   // halted — and runs again with the same index — marked no zone)
   if constexpr(PM == 2)
-    if(__builtin_amdgcn_readfirstlane(c_eng.zplan[z]) == sidx + 1u) return;
+    if(__builtin_amdgcn_readfirstlane(c_eng.zplan[z]) == sidx + 1u) return false;
   // One rank: a zone buffer overflowed into the spill list. The host grows the
   // zones and lands those records before another step runs; until then every
   // step is a no-op (spill_n[cur] is final for this launch; halt is set only
@@ -1201,15 +1242,15 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       c_eng.pend[pend_slot] = kPendSkipped;
       atomicAdd(c_eng.skipped, 1ull);
     }
-    return;
+    return false;
   }
 #ifdef GPA_STAMPS
   // the device's 100 MHz real-time clock (one for every XCD, unlike the
   // shader clock of GPA_STAMP): zone start [11] and end [12] across the grid
   if(tid == 0)
   {
-    c_eng.dbg[blockIdx.x * kDbgSlots + 11] = __builtin_amdgcn_s_memrealtime();
-    c_eng.dbg[blockIdx.x * kDbgSlots + 12] = 0;
+    c_eng.dbg[z * kDbgSlots + 11] = __builtin_amdgcn_s_memrealtime();
+    c_eng.dbg[z * kDbgSlots + 12] = 0;
   }
 #endif
   if(tid < GPU_ACTOR_MAX_TYPES) s_bytype[tid] = 0;
@@ -1250,7 +1291,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     c_eng.bigc_n[cur ^ 1u] = 0ull;
   }
   if constexpr(PM == 1)
-    if(gate || ztc != 0u || (kPlanSplit && c_eng.two_pass == 0u)) return;
+    if(gate || ztc != 0u || (kPlanSplit && c_eng.two_pass == 0u)) return false;
   uint8_t* const tb_out = c_eng.trig_own[nxt];
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
@@ -1264,7 +1305,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   const uint32_t nl = min(rfl(c_eng.land_n[cur][z]), cap);
   if(nc + nl == 0 && ztc == 0)
   {
-    if constexpr(PM == 1) return;
+    if constexpr(PM == 1) return false;
     // an idle zone (uniform: every thread read the same counters) has
     // nothing to count, run or send — the quiet tail of a run, or zones of
     // a sparse workload; it only clears trigger bytes it left two steps ago
@@ -1274,10 +1315,10 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       for(uint32_t i = tid; i < nact; i += kZoneThreads) tb_out[(L0 + i) * R + me] = 0;
       if(tid == 0) c_eng.ztrig[nxt][z] = 0;
     }
-    return;
+    return false;
   }
   if constexpr(kSimple)
-    if(nc != 0u || nl > kIdxCap) return;
+    if(nc != 0u || nl > kIdxCap) return false;
   // the trigger bytes of this zone's actors as the last step left them
   if(ztc)
     for(uint32_t i = tid; i < kZone; i += kZoneThreads)
@@ -1349,7 +1390,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
       tz = (int)t;
   tz = __builtin_amdgcn_readfirstlane(tz);
   if constexpr(PM == 1)
-    if(tz < 0) return;
+    if(tz < 0) return false;
   // A zone of a two-pass table that may take that path (no backpressure
   // anywhere, one type) loads its actors' state now, coalesced, so that the
   // loads land while the landing buffer is counted; dropped if it does not.
@@ -1467,13 +1508,13 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
   {
     if constexpr(kPlanSplit)
     {
-      if(!plan) return;                         // uniform: left to PM 2
+      if(!plan) return false;                         // uniform: left to PM 2
     }
     else
     {
       int big = 0;
       for(uint32_t i = tid; i < kZone; i += kZoneThreads) big |= s_cnt[i] > kBigGroup;
-      if(__syncthreads_or(big)) return;         // a hot group: left to PM 2
+      if(__syncthreads_or(big)) return false;         // a hot group: left to PM 2
     }
     take_mail();
   }
@@ -1710,7 +1751,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
           st[r][k] = s_stage[k * kZone + ai[r]];
 #ifdef GPA_STAMPS
       GPA_STAMP(8);                           // the permuted state is in registers
-      if(tid == 0) { c_eng.dbg[blockIdx.x * kDbgSlots + 9] = 0; c_eng.dbg[blockIdx.x * kDbgSlots + 10] = 0; }
+      if(tid == 0) { c_eng.dbg[z * kDbgSlots + 9] = 0; c_eng.dbg[z * kDbgSlots + 10] = 0; }
 #endif
       // pass 1: count the sends of each round per bucket
 #pragma unroll
@@ -1894,7 +1935,7 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
             T.state[(size_t)k * T.lcount + (L0 + i - T.lfirst)] = s_stage[k * kZone + i];
       }
 #ifdef GPA_STAMPS
-      if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 2] = emit_clk;
+      if(tid == 0) c_eng.dbg[z * kDbgSlots + 2] = emit_clk;
 #endif
       sent = tc.sent;
       xover += tc.xover;
@@ -2345,8 +2386,36 @@ __global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t
     if constexpr(PM == 1) c_eng.zplan[z] = sidx + 1u;
   }
 #ifdef GPA_STAMPS
-  if(tid == 0) c_eng.dbg[blockIdx.x * kDbgSlots + 12] = __builtin_amdgcn_s_memrealtime();
+  if(tid == 0) c_eng.dbg[z * kDbgSlots + 12] = __builtin_amdgcn_s_memrealtime();
 #endif
+  return true;
+}
+
+
+// The general path of PM 3 (below) as a call: its registers apart from the
+// two-pass path's (inlined beside it, the plan path spills and runs slower:
+// profiles/r05s_split_pass2_ab.txt, one launch 107 us against 72.5)
+template <int HTS>
+__device__ __noinline__ void zone_step_rest(uint32_t z, uint32_t cur, uint32_t pend_slot, uint32_t sidx)
+{
+  zone_step<HTS, 2>(z, cur, pend_slot, sidx);
+}
+
+// One workgroup per zone. PM 3 (split tables): the step as one launch —
+// PM 1's path, and for a zone it leaves, PM 2's through the call above
+// (nothing is written before PM 1 leaves a zone, so PM 2 starts it afresh;
+// the zone is unmarked, so PM 2 does not return at its mark).
+template <int HTS, int PM>
+__global__ void __launch_bounds__(kZoneThreads, 4) k_step(uint32_t cur, uint32_t pend_slot,
+  uint32_t sidx)
+{
+  if constexpr(PM != 3)
+    zone_step<HTS, PM>(blockIdx.x, cur, pend_slot, sidx);
+  else if(!zone_step<HTS, 1>(blockIdx.x, cur, pend_slot, sidx))
+  {
+    __syncthreads();                     // PM 1's LDS reads are done
+    zone_step_rest<HTS>(blockIdx.x, cur, pend_slot, sidx);
+  }
 }
 
 // The helper kernels below belong to engine.hip's code object only (the

@@ -1,11 +1,12 @@
 """GPU parity of the step run as one launch or as two.
 
-A two-pass table's step (the message-ubench pinger) is two launches by default
-(zone_dev.h k_step PM 1: the zones that take the two passes; PM 2: the rest,
-on the general path); so is C2-det's and the storm's (PM 1: the plain zones —
-no carried mail, no backpressure, no group over kBigGroup; PM 2: the rest).
-PONYC_AMD_SPLIT_PLAN=0 runs the one-launch kernel (PM 0). Both must equal the
-oracle: steps where every zone takes PM 1, steps where the batch limit, carried
+A two-pass table's step (the message-ubench pinger) is split (zone_dev.h k_step
+PM 1: the zones that take the two passes; PM 2: the rest, on the general
+path), by default as one launch that calls PM 2's code for the zones PM 1
+leaves (PM 3; PONYC_AMD_FUSE=0: two launches); C2-det's and the storm's are two
+launches (PM 1: the plain zones — no carried mail, no backpressure, no group
+over kBigGroup; PM 2: the rest). PONYC_AMD_SPLIT_PLAN=0 runs the unsplit kernel
+(PM 0). Every form must equal the oracle: steps where every zone takes PM 1, steps where the batch limit, carried
 mail or a hot group send zones to PM 2, and a forward budget whose ramp-down
 mixes the two in one step — at both zone geometries."""
 import numpy as np
@@ -32,19 +33,26 @@ CASES = {
 }
 
 
+FORMS = {"unsplit": ("0", "1"), "two_launches": ("1", "0"), "fused": ("1", "1")}
+
+
 @pytest.mark.parametrize("bits", ["11", "12"])
-@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("name", list(CASES))
-def test_split_launch(engine_factory, oracle, monkeypatch, name, split, bits):
+def test_split_launch(engine_factory, oracle, monkeypatch, name, form, bits):
+    if form == "fused" and not name.startswith("ubench"):
+        pytest.skip("PM 3 is built for the two-pass table only (step_tu.h split_kernel)")
+    split, fuse = FORMS[form]
     monkeypatch.setenv("PONYC_AMD_SPLIT_PLAN", split)
+    monkeypatch.setenv("PONYC_AMD_FUSE", fuse)
     monkeypatch.setenv("PONYC_AMD_ZONE_BITS", bits)
     setup, result = CASES[name]
     g, o = _both(engine_factory, oracle, setup, result)
     _assert_same(g, o)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_trigger_slots_clear_after_triggers_stop(engine_factory, oracle, monkeypatch, split):
+@pytest.mark.parametrize("form", list(FORMS))
+def test_trigger_slots_clear_after_triggers_stop(engine_factory, oracle, monkeypatch, form):
     """trig_n (zone_dev.h: read step s's slot, add to s+1's, clear s+2's) goes
     back to 0 once no actor triggers muting — also when zone 0 of the clearing
     step runs in the split's first launch (PM 1 never cleared it,
@@ -52,7 +60,9 @@ def test_trigger_slots_clear_after_triggers_stop(engine_factory, oracle, monkeyp
     pings make actor 0 run a full batch in step 0 (overloaded: a trigger, the
     oracle's trig_count); no actor triggers after that, while the budgeted
     pings drain over five more steps in which every zone plans."""
+    split, fuse = FORMS[form]
     monkeypatch.setenv("PONYC_AMD_SPLIT_PLAN", split)
+    monkeypatch.setenv("PONYC_AMD_FUSE", fuse)
 
     def setup(e):
         w = W.ubench(e, 4096, 3, 6)
