@@ -511,8 +511,9 @@ def main():
                 "traffic_source": traffic_src,
                 # a two-pass table's step is two launches (zone_dev.h k_step PM
                 # 1 and 2); the events span both
-                "kernel": ("k_step" if os.environ.get("PONYC_AMD_SPLIT_PLAN") == "0"
-                           else "k_step<PINGER,1> + k_step<PINGER,2>"),
+                "kernel": ("k_step<PINGER,0>" if os.environ.get("PONYC_AMD_SPLIT_PLAN") == "0"
+                           else "k_step<PINGER,1> + k_step<PINGER,2>" if os.environ.get("PONYC_AMD_FUSE") == "0"
+                           else "k_step<PINGER,3> (one launch: the two-pass path, the rest through a call)"),
                 "kernel_ms": round(step_ms, 5),
                 "kernel_ms_source": "HIP events around the timed launches on the engine stream, / steps",
                 "alg_bytes_per_launch": round(alg_bytes, 1),
