@@ -772,10 +772,16 @@ template <class A>
 __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SINK>, const TypeDev& T, A& a,
   uint64_t (&s)[11], uint32_t beh, uint64_t arg)
 {
-  // slot = ((arg >> 32) / ns) % 8, in 32-bit arithmetic (the sender index
-  // is 32 bits; a 64-bit division was most of a hot sink's per-message cost)
-  const uint64_t ns = T.params[0] ? T.params[0] : 1;
-  const uint32_t slot = ns > 0xFFFFFFFFull ? 0u : (((uint32_t)(arg >> 32) / (uint32_t)ns) & 7u);
+  // slot = ((arg >> 32) / ns) % 8. The sender index is 32 bits, so the
+  // quotient is mulhi(floor(2^64 / ns) + 1, index) for ns >= 2 (rdiv's
+  // fastdiv); the magic depends on the type's parameter only and leaves the
+  // drain's loop (a 64-bit and then a 32-bit division per message were most of
+  // a hot sink's per-behaviour instructions)
+  const uint64_t ns = T.params[0] > 1 ? T.params[0] : 1;
+  const uint64_t magic = ~0ull / ns + 1u;
+  const uint32_t sx = (uint32_t)(arg >> 32);
+  const uint32_t slot = ns > 0xFFFFFFFFull ? 0u
+                      : ((ns == 1 ? sx : (uint32_t)__umul64hi(magic, (uint64_t)sx)) & 7u);
   const uint64_t seq = arg & 0xFFFFFFFFull;
   s[1] += 1;
   s[0] = (s[0] ^ arg) * 0x100000001b3ull;
