@@ -140,6 +140,14 @@ GPU_ACTOR_API int gpu_actor_type_priority(uint32_t type_id, int32_t priority);
 /* Handler-table parameter `idx` (< GPU_ACTOR_MAX_PARAMS) of a type; set before
  * gpu_actor_create, which runs the table's constructor with them. */
 GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
+/* The behaviours of a GPU_ACTOR_HT_PROGRAM type, given at run time: `n`
+ * instruction words (below), copied to the device. Replaces the generated
+ * per-type dispatch switch (src/libponyc/codegen/gentype.c:358-395, the
+ * pony_type_t.dispatch the runtime calls in actor.c:437-480) for behaviour
+ * sets the compiled tables do not hold — no library rebuild. Any time while
+ * no run is in flight; an engine that holds programs runs them on the zone
+ * path (never the small-step path). */
+GPU_ACTOR_API int gpu_actor_type_program(uint32_t type_id, const uint64_t* code, uint32_t n);
 
 /* ---- actors (pony_create, actor.c:688-734) ------------------------------ */
 /* Bulk-create `count` actors of a type (once per type); ids are
@@ -325,6 +333,42 @@ GPU_ACTOR_API const char* gpu_actor_strerror(int code);
 #define GPU_ACTOR_HT_SPREADER        11
 #define GPU_ACTOR_SPREADER_SPREAD    0
 #define GPU_ACTOR_SPREADER_RESULT    1
+
+/* 12: behaviours as a program (gpu_actor_type_program), interpreted per
+ * message. state: 8 words. Registers r0-r7 are the state words, r8 the
+ * message argument, r9 the actor's id, r10 the behaviour, r11-r15 zero at
+ * entry; r0-r7 are the state afterwards. Words 0-15 of the program are the
+ * entry index of behaviour 0-15's code (0: the behaviour does nothing); code
+ * follows. An instruction is one u64:
+ *   op | d << 8 | a << 12 | b << 16 | (uint32_t)imm << 32   (imm: int32)
+ * and pc indexes the next instruction while one runs. A behaviour ends at
+ * HALT, at an invalid op or pc, or after GPU_ACTOR_PROG_MAX_STEPS
+ * instructions. SEND to an id past the world's ids is dropped (counted).   */
+#define GPU_ACTOR_HT_PROGRAM         12
+#define GPU_ACTOR_PROG_ENTRIES       16
+#define GPU_ACTOR_PROG_MAX_STEPS     4096
+#define GPU_ACTOR_OP_HALT   0   /* end the behaviour                          */
+#define GPU_ACTOR_OP_LDI    1   /* r[d] = (int64)imm                          */
+#define GPU_ACTOR_OP_LDP    2   /* r[d] = type param (imm & 7)                */
+#define GPU_ACTOR_OP_MOV    3   /* r[d] = r[a]                                */
+#define GPU_ACTOR_OP_ADD    4   /* r[d] = r[a] + r[b]                         */
+#define GPU_ACTOR_OP_SUB    5   /* r[d] = r[a] - r[b]                         */
+#define GPU_ACTOR_OP_MUL    6   /* r[d] = r[a] * r[b] (low 64 bits)           */
+#define GPU_ACTOR_OP_MULHI  7   /* r[d] = (r[a] * r[b]) >> 64, unsigned       */
+#define GPU_ACTOR_OP_AND    8
+#define GPU_ACTOR_OP_OR     9
+#define GPU_ACTOR_OP_XOR    10
+#define GPU_ACTOR_OP_SHL    11  /* r[d] = r[a] << (r[b] & 63)                 */
+#define GPU_ACTOR_OP_SHR    12  /* r[d] = r[a] >> (r[b] & 63), logical        */
+#define GPU_ACTOR_OP_ADDI   13  /* r[d] = r[a] + (int64)imm                   */
+#define GPU_ACTOR_OP_LTU    14  /* r[d] = r[a] < r[b] (unsigned), 0 or 1      */
+#define GPU_ACTOR_OP_EQ     15  /* r[d] = r[a] == r[b], 0 or 1                */
+#define GPU_ACTOR_OP_JZ     16  /* if r[a] == 0: pc += imm                    */
+#define GPU_ACTOR_OP_JNZ    17  /* if r[a] != 0: pc += imm                    */
+#define GPU_ACTOR_OP_JMP    18  /* pc += imm                                  */
+#define GPU_ACTOR_OP_SEND   19  /* send behaviour (imm & 15), arg r[b], to r[a] */
+#define GPU_ACTOR_OP_MIX    20  /* r[d] = splitmix64 finaliser of r[a]        */
+#define GPU_ACTOR_OP_YIELD  21  /* end this actor's run after this behaviour  */
 
 #define GPU_ACTOR_NONE 0xFFFFFFFFFFFFFFFFULL
 

@@ -55,6 +55,8 @@ typedef struct {
   uint64_t reserve;       /* room for actors spawned by behaviours           */
   uint64_t* state;        /* field-major: state[w * count + i] */
   uint64_t delivered;
+  uint64_t* prog;         /* GPU_ACTOR_HT_PROGRAM: the behaviours' program */
+  uint32_t prog_n;
 } otype_t;
 
 /* an actor created by a behaviour this step: id assigned at the step's end */
@@ -103,7 +105,10 @@ int or_init(uint32_t n_types_max)
 void or_shutdown(void)
 {
   for(int t = 0; t < GPU_ACTOR_MAX_TYPES; t++)
+  {
     free(S.types[t].state);
+    free(S.types[t].prog);
+  }
   for(uint64_t a = 0; a < S.n_actors; a++)
     free(S.mb[a].buf);
   free(S.mb);
@@ -132,7 +137,8 @@ int or_type_live(uint32_t type_id, uint64_t* out)
 
 int or_type_register(uint32_t type_id, uint32_t state_words, uint32_t ht)
 {
-  if(!S.init || type_id >= GPU_ACTOR_MAX_TYPES || ht < 1 || ht > 11) return GPU_ACTOR_EINVAL;
+  if(!S.init || type_id >= GPU_ACTOR_MAX_TYPES || ht < 1 || ht > GPU_ACTOR_HT_PROGRAM) return GPU_ACTOR_EINVAL;
+  if(ht == GPU_ACTOR_HT_PROGRAM && state_words < 8) return GPU_ACTOR_EINVAL;
   otype_t* t = &S.types[type_id];
   if(t->registered) return GPU_ACTOR_EINVAL;
   t->registered = 1;
@@ -158,6 +164,21 @@ int or_type_priority(uint32_t type_id, int32_t priority)
 {
   if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered) return GPU_ACTOR_EINVAL;
   S.types[type_id].priority = priority;
+  return 0;
+}
+
+/* gpu_actor_type_program: the behaviours of a GPU_ACTOR_HT_PROGRAM type */
+int or_type_program(uint32_t type_id, const uint64_t* code, uint32_t n)
+{
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !S.types[type_id].registered ||
+     S.types[type_id].ht != GPU_ACTOR_HT_PROGRAM || !code || n <= GPU_ACTOR_PROG_ENTRIES ||
+     n > (1u << 20)) return GPU_ACTOR_EINVAL;
+  uint64_t* p = malloc((size_t)n * sizeof(uint64_t));
+  if(!p) return GPU_ACTOR_ENOMEM;
+  memcpy(p, code, (size_t)n * sizeof(uint64_t));
+  free(S.types[type_id].prog);
+  S.types[type_id].prog = p;
+  S.types[type_id].prog_n = n;
   return 0;
 }
 
@@ -398,6 +419,57 @@ static void place_spawns(void)
 }
 
 /* ---- behaviours ---------------------------------------------------------- */
+/* GPU_ACTOR_HT_PROGRAM (include/gpu_actor.h): one behaviour of the type's
+ * program; w0 points at state word 0, word k at w0[k * stride]. */
+static void run_program(const otype_t* t, uint64_t self, uint32_t beh, uint64_t arg,
+  uint64_t* w0, uint64_t stride)
+{
+  const uint64_t* P = t->prog;
+  const uint32_t np = t->prog_n;
+  if(!P || np <= GPU_ACTOR_PROG_ENTRIES) return;
+  uint32_t pc = (uint32_t)P[beh & 15];
+  if(pc == 0) return;
+  uint64_t r[16] = {0};
+  for(int k = 0; k < 8; k++) r[k] = w0[(uint64_t)k * stride];
+  r[8] = arg; r[9] = self; r[10] = beh;
+  for(uint32_t step = 0; step < GPU_ACTOR_PROG_MAX_STEPS && pc < np; step++)
+  {
+    const uint64_t ins = P[pc++];
+    const uint32_t op = (uint32_t)(ins & 0xFF), d = (uint32_t)(ins >> 8) & 15;
+    const uint64_t x = r[(ins >> 12) & 15], y = r[(ins >> 16) & 15];
+    const int64_t imm = (int32_t)(uint32_t)(ins >> 32);
+    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_YIELD) break;
+    switch(op)
+    {
+      case GPU_ACTOR_OP_JZ:    if(x == 0) pc = (uint32_t)((int64_t)pc + imm); continue;
+      case GPU_ACTOR_OP_JNZ:   if(x != 0) pc = (uint32_t)((int64_t)pc + imm); continue;
+      case GPU_ACTOR_OP_JMP:   pc = (uint32_t)((int64_t)pc + imm); continue;
+      case GPU_ACTOR_OP_SEND:
+        if(x < S.n_actors) send(x, (uint32_t)imm & 15, y);
+        else S.dropped++;
+        continue;
+      case GPU_ACTOR_OP_YIELD: S.yield_req = 1; continue;
+      case GPU_ACTOR_OP_LDI:   r[d] = (uint64_t)imm; break;
+      case GPU_ACTOR_OP_LDP:   r[d] = t->params[imm & 7]; break;
+      case GPU_ACTOR_OP_MOV:   r[d] = x; break;
+      case GPU_ACTOR_OP_ADD:   r[d] = x + y; break;
+      case GPU_ACTOR_OP_SUB:   r[d] = x - y; break;
+      case GPU_ACTOR_OP_MUL:   r[d] = x * y; break;
+      case GPU_ACTOR_OP_MULHI: r[d] = or_mulhi(x, y); break;
+      case GPU_ACTOR_OP_AND:   r[d] = x & y; break;
+      case GPU_ACTOR_OP_OR:    r[d] = x | y; break;
+      case GPU_ACTOR_OP_XOR:   r[d] = x ^ y; break;
+      case GPU_ACTOR_OP_SHL:   r[d] = x << (y & 63); break;
+      case GPU_ACTOR_OP_SHR:   r[d] = x >> (y & 63); break;
+      case GPU_ACTOR_OP_ADDI:  r[d] = x + (uint64_t)imm; break;
+      case GPU_ACTOR_OP_LTU:   r[d] = x < y; break;
+      case GPU_ACTOR_OP_EQ:    r[d] = x == y; break;
+      default:                 r[d] = or_splitmix_mix(x); break;     /* GPU_ACTOR_OP_MIX */
+    }
+  }
+  for(int k = 0; k < 8; k++) w0[(uint64_t)k * stride] = r[k];
+}
+
 static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
 {
   uint64_t n = t->count, i = self - t->first;
@@ -530,6 +602,10 @@ static void handle(otype_t* t, uint64_t self, uint32_t beh, uint64_t arg)
           else W(4) = W(2) + 1;                    /* print(_result + 1 " actors") */
         }
       }
+      break;
+
+    case GPU_ACTOR_HT_PROGRAM:
+      run_program(t, self, beh, arg, &W(0), n);
       break;
 
     case GPU_ACTOR_HT_FIFO_SINK: {

@@ -61,6 +61,7 @@ int  or_type_register(uint32_t type_id, uint32_t state_words, uint32_t ht);
 int  or_type_config(uint32_t type_id, uint32_t batch, uint32_t mailbox_cap);
 int  or_type_priority(uint32_t type_id, int32_t priority);
 int  or_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
+int  or_type_program(uint32_t type_id, const uint64_t* code, uint32_t n);
 int  or_create(uint32_t type_id, uint64_t count, uint64_t* first_id);
 /* room for n actors created by behaviours (before or_create); live count */
 int  or_type_reserve(uint32_t type_id, uint64_t n);

@@ -47,6 +47,7 @@ def load():
         "or_type_config": (i32, [u32, u32, u32]),
         "or_type_priority": (i32, [u32, ctypes.c_int32]),
         "or_type_param": (i32, [u32, u32, u64]),
+        "or_type_program": (i32, [u32, vp, u32]),
         "or_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
         "or_type_reserve": (i32, [u32, u64]),
         "or_type_live": (i32, [u32, ctypes.POINTER(u64)]),
@@ -106,6 +107,10 @@ class Oracle:
 
     def type_param(self, type_id, idx, value):
         _ck("or_type_param", self.lib.or_type_param(type_id, idx, int(value) & U64))
+
+    def type_program(self, type_id, code):
+        c = np.ascontiguousarray(code, dtype=np.uint64)
+        _ck("or_type_program", self.lib.or_type_program(type_id, c.ctypes.data, c.size))
 
     def type_reserve(self, type_id, n):
         _ck("or_type_reserve", self.lib.or_type_reserve(type_id, n))

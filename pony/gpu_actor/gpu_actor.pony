@@ -23,6 +23,7 @@ use @gpu_actor_type_register[I32](type_id: U32, state_words: U32, table: U32)
 use @gpu_actor_type_config[I32](type_id: U32, batch: U32, mailbox_cap: U32)
 use @gpu_actor_type_priority[I32](type_id: U32, priority: I32)
 use @gpu_actor_type_param[I32](type_id: U32, idx: U32, value: U64)
+use @gpu_actor_type_program[I32](type_id: U32, code: Pointer[U64] tag, n: U32)
 use @gpu_actor_create[I32](type_id: U32, count: U64, first: Pointer[U64])
 use @gpu_actor_type_reserve[I32](type_id: U32, n: U64)
 use @gpu_actor_type_live[I32](type_id: U32, live: Pointer[U64])

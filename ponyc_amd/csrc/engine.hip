@@ -40,6 +40,7 @@ StepEntry step_entry_gups_streamer();
 StepEntry step_entry_storm();
 StepEntry step_entry_spreader();
 StepEntry step_entry_fifo_pair();
+StepEntry step_entry_program();
 } // namespace gpa_z12
 
 using namespace gpa;
@@ -273,6 +274,8 @@ struct HostType {
   uint64_t reserve = 0;                 // ids for actors spawned by behaviours
   int32_t priority = 0;                 // the fork's _priority() hint
   uint64_t* d_state = nullptr;
+  uint64_t* d_prog = nullptr;           // GPU_ACTOR_HT_PROGRAM: the behaviours' program
+  uint32_t prog_n = 0;
 };
 
 struct Engine {
@@ -458,7 +461,8 @@ const std::vector<StepEntry>& step_entries()
     gpa_z12::step_entry_any(), gpa_z12::step_entry_ring(), gpa_z12::step_entry_pinger(),
     gpa_z12::step_entry_pinger_det(), gpa_z12::step_entry_fanin_sender(),
     gpa_z12::step_entry_gups_streamer(), gpa_z12::step_entry_storm(),
-    gpa_z12::step_entry_spreader(), gpa::step_entry_fifo_pair(), gpa_z12::step_entry_fifo_pair()};
+    gpa_z12::step_entry_spreader(), gpa::step_entry_fifo_pair(), gpa_z12::step_entry_fifo_pair(),
+    gpa::step_entry_program(), gpa_z12::step_entry_program()};
   return v;
 }
 
@@ -500,6 +504,8 @@ int upload_types()
     d.prio = h.priority > 0 ? 1u : 0u;
     d.state = h.d_state;
     memcpy(d.params, h.params, sizeof(d.params));
+    d.prog = h.d_prog;
+    d.prog_n = h.prog_n;
   }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_types), td, sizeof(td), 0,
     hipMemcpyHostToDevice, g.stream));
@@ -507,6 +513,7 @@ int upload_types()
   memset(&e, 0, sizeof(e));
   e.n_types = g.n_types; e.rank = rank(); e.nranks = R(); e.n_local = g.n_local;
   e.n_zones = g.n_zones; e.zoff = g.d_zoff; e.zcapz = g.d_zcap;
+  e.n_ids = (uint32_t)std::min<uint64_t>(g.n_actors, 0xFFFFFFFFull);
   e.r_magic = R() > 1 ? ~0ull / R() + 1 : 0;
   for(int p = 0; p < 2; ++p)
   {
@@ -877,6 +884,7 @@ uint32_t required_words(uint32_t ht)
     case GPU_ACTOR_HT_FIFO_SRC: return 3;
     case GPU_ACTOR_HT_FIFO_SINK: return 11;
     case GPU_ACTOR_HT_SPREADER: return 5;
+    case GPU_ACTOR_HT_PROGRAM: return 8;
     default: return 0;
   }
 }
@@ -1321,6 +1329,7 @@ StepEntry step_entry_for(bool z12)
       return z12 ? gpa_z12::step_entry_gups_streamer() : gpa::step_entry_gups_streamer();
     case GPU_ACTOR_HT_STORM: return z12 ? gpa_z12::step_entry_storm() : gpa::step_entry_storm();
     case GPU_ACTOR_HT_SPREADER: return z12 ? gpa_z12::step_entry_spreader() : gpa::step_entry_spreader();
+    case GPU_ACTOR_HT_PROGRAM: return z12 ? gpa_z12::step_entry_program() : gpa::step_entry_program();
     default: return z12 ? gpa_z12::step_entry_any() : gpa::step_entry_any();
   }
 }
@@ -1584,7 +1593,10 @@ int ensure_events(size_t n)
 void free_all()
 {
   for(auto& t : g.types)
+  {
     if(t.d_state) (void)hipFree(t.d_state);
+    if(t.d_prog) (void)hipFree(t.d_prog);
+  }
   for(int p = 0; p < 2; ++p)
   {
     if(g.d_land[p]) (void)hipFree(g.d_land[p]);
@@ -2002,6 +2014,28 @@ GPU_ACTOR_API int gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t 
     !g.types[type_id].registered) return GPU_ACTOR_EINVAL;
   g.types[type_id].params[idx] = value;
   return g.types[type_id].created ? upload_types() : 0;
+}
+
+GPU_ACTOR_API int gpu_actor_type_program(uint32_t type_id, const uint64_t* code, uint32_t n)
+{
+  std::lock_guard<std::mutex> lk(g.mu);
+  if(!g.init) return GPU_ACTOR_ESTATE;
+  if(type_id >= GPU_ACTOR_MAX_TYPES || !g.types[type_id].registered ||
+     g.types[type_id].ht != GPU_ACTOR_HT_PROGRAM || !code || n <= GPU_ACTOR_PROG_ENTRIES ||
+     n > (1u << 20)) return GPU_ACTOR_EINVAL;
+  if(g.async_busy) return GPU_ACTOR_EBUSY;
+  HostType& t = g.types[type_id];
+  uint64_t* d = nullptr;
+  HIPCK(hipMalloc(&d, (size_t)n * sizeof(uint64_t)));
+  HIPCK(hipMemcpy(d, code, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice));
+  if(t.d_prog)
+  {
+    HIPCK(hipStreamSynchronize(g.stream));          // no launch still reads the old one
+    HIPCK(hipFree(t.d_prog));
+  }
+  t.d_prog = d;
+  t.prog_n = n;
+  return t.created ? upload_types() : 0;
 }
 
 GPU_ACTOR_API int gpu_actor_create(uint32_t type_id, uint64_t count, uint64_t* first_id)

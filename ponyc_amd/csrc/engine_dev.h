@@ -117,6 +117,8 @@ struct TypeDev {
   uint32_t reducible, prio;   // prio: priority > 0 (gpu_actor_type_priority)
   uint64_t* state;           // [words][lcount]
   uint64_t  params[GPU_ACTOR_MAX_PARAMS];
+  const uint64_t* prog;      // GPU_ACTOR_HT_PROGRAM: the behaviours' program
+  uint32_t  prog_n, prog_pad;
 };
 
 // One deferred carry copy: records rec(from + j), j < rem, of an actor's
@@ -136,7 +138,8 @@ static_assert(sizeof(BigCopy) == 48, "BigCopy is 48 B");
 
 struct EngDev {
   uint32_t n_types, rank, nranks, n_local;
-  uint32_t n_zones, pad0;
+  uint32_t n_zones;
+  uint32_t n_ids;                 // the world's actor ids (SEND of a program past them drops)
   uint64_t r_magic;               // floor(2^64 / nranks) + 1 (nranks > 1): rdiv
   const uint64_t* zoff;           // [n_zones] record offset of each zone's buffers
   const uint32_t* zcapz;          // [n_zones] records a zone buffer holds
@@ -644,6 +647,7 @@ template <> struct HT_Words<GPU_ACTOR_HT_STORM>         { static constexpr int W
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SRC>      { static constexpr int W = 3; };
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SINK>     { static constexpr int W = 11; };
 template <> struct HT_Words<GPU_ACTOR_HT_SPREADER>      { static constexpr int W = 5; };
+template <> struct HT_Words<GPU_ACTOR_HT_PROGRAM>       { static constexpr int W = 8; };
 
 template <int HT> struct HtTag {};
 
@@ -794,6 +798,74 @@ __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_FIFO_SINK>, const Type
   for(int k = 0; k < 8; ++k) s[3 + k] = (slot == (uint32_t)k) ? seq : s[3 + k];
   // param 1: yield after every k-th message
   if(T.params[1] && s[1] % T.params[1] == 0) actor_yield(a);
+}
+
+// Behaviours as a program (include/gpu_actor.h GPU_ACTOR_HT_PROGRAM): the
+// reference's generated dispatch (gentype.c:358-395) for any behaviour set,
+// here one interpreter lane per actor. Registers r0-r7 are the state, r8 the
+// argument, r9 self, r10 the behaviour; indexed at run time, they live in
+// scratch. oracle/bsp.c restates it instruction for instruction.
+template <class A>
+__device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_PROGRAM>, const TypeDev& T, A& a,
+  uint64_t (&s)[8], uint32_t beh, uint64_t arg)
+{
+  const uint64_t* const P = T.prog;
+  const uint32_t np = T.prog_n;
+  if(!P || np <= GPU_ACTOR_PROG_ENTRIES) return;
+  uint32_t pc = (uint32_t)P[beh & 15u];
+  if(pc == 0) return;
+  uint64_t r[16];
+#pragma unroll
+  for(int k = 0; k < 8; ++k) r[k] = s[k];
+  r[8] = arg; r[9] = a.self; r[10] = beh;
+#pragma unroll
+  for(int k = 11; k < 16; ++k) r[k] = 0;
+  for(uint32_t step = 0; step < GPU_ACTOR_PROG_MAX_STEPS && pc < np; ++step)
+  {
+    const uint64_t ins = P[pc++];
+    const uint32_t op = (uint32_t)ins & 0xFFu, d = ((uint32_t)ins >> 8) & 15u;
+    const uint64_t x = r[((uint32_t)ins >> 12) & 15u], y = r[((uint32_t)ins >> 16) & 15u];
+    const int64_t imm = (int32_t)(uint32_t)(ins >> 32);
+    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_YIELD) break;
+    if(op == GPU_ACTOR_OP_JZ || op == GPU_ACTOR_OP_JNZ || op == GPU_ACTOR_OP_JMP)
+    {
+      const bool take = op == GPU_ACTOR_OP_JMP || ((x == 0) == (op == GPU_ACTOR_OP_JZ));
+      if(take) pc = (uint32_t)((int64_t)pc + imm);
+      continue;
+    }
+    if(op == GPU_ACTOR_OP_SEND)
+    {
+      if(x < c_eng.n_ids)
+        send_serial(a, (uint32_t)x, (uint32_t)imm & 15u, y);
+      else
+        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+      continue;
+    }
+    if(op == GPU_ACTOR_OP_YIELD) { actor_yield(a); continue; }
+    uint64_t v;
+    switch(op)
+    {
+      case GPU_ACTOR_OP_LDI:   v = (uint64_t)imm; break;
+      case GPU_ACTOR_OP_LDP:   v = T.params[imm & 7]; break;
+      case GPU_ACTOR_OP_MOV:   v = x; break;
+      case GPU_ACTOR_OP_ADD:   v = x + y; break;
+      case GPU_ACTOR_OP_SUB:   v = x - y; break;
+      case GPU_ACTOR_OP_MUL:   v = x * y; break;
+      case GPU_ACTOR_OP_MULHI: v = __umul64hi(x, y); break;
+      case GPU_ACTOR_OP_AND:   v = x & y; break;
+      case GPU_ACTOR_OP_OR:    v = x | y; break;
+      case GPU_ACTOR_OP_XOR:   v = x ^ y; break;
+      case GPU_ACTOR_OP_SHL:   v = x << (y & 63u); break;
+      case GPU_ACTOR_OP_SHR:   v = x >> (y & 63u); break;
+      case GPU_ACTOR_OP_ADDI:  v = x + (uint64_t)imm; break;
+      case GPU_ACTOR_OP_LTU:   v = x < y ? 1u : 0u; break;
+      case GPU_ACTOR_OP_EQ:    v = x == y ? 1u : 0u; break;
+      default:                 v = splitmix_mix(x); break;     // GPU_ACTOR_OP_MIX
+    }
+    r[d] = v;
+  }
+#pragma unroll
+  for(int k = 0; k < 8; ++k) s[k] = r[k];
 }
 
 // examples/spreader/main.pony:9-48

@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     s_tinfo[tid].lcount = T.lcount;
     s_tinfo[tid].batch = T.batch;
     // reducible types never run; spawning and yielding ones need the zone path
-    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER ||
+    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER || T.ht == GPU_ACTOR_HT_PROGRAM ||
                           (T.ht == GPU_ACTOR_HT_FIFO_SINK && T.params[1] != 0)) ? kSpNoRun : 0u;
   }
   if(tid == 0) { sp_cnt[0] = 0; sp_cnt[1] = 0; s_over = 0; }

@@ -43,5 +43,6 @@ StepEntry step_entry_gups_streamer();
 StepEntry step_entry_storm();
 StepEntry step_entry_spreader();
 StepEntry step_entry_fifo_pair();       // FIFO sources + sinks (zone_dev.h kHtFifoPair)
+StepEntry step_entry_program();         // behaviours as programs (GPU_ACTOR_HT_PROGRAM)
 
 } // namespace gpa

@@ -382,7 +382,7 @@ template <int HT> __host__ __device__ constexpr uint32_t seq_batch()
 
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
-  return HT == GPU_ACTOR_HT_FIFO_SINK;
+  return HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_PROGRAM;
 }
 
 // Drain one actor: handle up to min(batch, n) messages — carried mail, then
@@ -2083,6 +2083,7 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
         ZCASE(GPU_ACTOR_HT_FIFO_SRC)
         ZCASE(GPU_ACTOR_HT_FIFO_SINK)
         ZCASE(GPU_ACTOR_HT_SPREADER)
+        ZCASE(GPU_ACTOR_HT_PROGRAM)
 #undef ZCASE
         default: break;
       }

@@ -31,6 +31,7 @@ GUPS_APPLY, GUPS_UPDATE = 0, 0
 STORM_TOKEN, STORM_STORM = 0, 1
 FIFO_BURST, FIFO_PUSH = 0, 0
 HT_SPREADER = 11
+HT_PROGRAM = 12                 # behaviours as programs (ponyc_amd.program)
 SPREADER_SPREAD, SPREADER_RESULT = 0, 1
 NONE_ID = 0xFFFFFFFFFFFFFFFF
 
@@ -77,7 +78,7 @@ class Counts(ctypes.Structure):
 EXPORTS = [
     "gpu_actor_init", "gpu_actor_shutdown", "gpu_actor_comm_id",
     "gpu_actor_type_register", "gpu_actor_type_config", "gpu_actor_type_priority",
-    "gpu_actor_type_param",
+    "gpu_actor_type_param", "gpu_actor_type_program",
     "gpu_actor_create", "gpu_actor_type_reserve", "gpu_actor_type_live",
     "gpu_actor_alloc_msgs", "gpu_actor_sendv", "gpu_actor_send",
     "gpu_actor_run", "gpu_actor_run_fixed", "gpu_actor_sync",
@@ -119,6 +120,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "gpu_actor_type_config": (i32, [u32, u32, u32]),
         "gpu_actor_type_priority": (i32, [u32, ctypes.c_int32]),
         "gpu_actor_type_param": (i32, [u32, u32, u64]),
+        "gpu_actor_type_program": (i32, [u32, vp, u32]),
         "gpu_actor_create": (i32, [u32, u64, ctypes.POINTER(u64)]),
         "gpu_actor_type_reserve": (i32, [u32, u64]),
         "gpu_actor_type_live": (i32, [u32, ctypes.POINTER(u64)]),
@@ -252,6 +254,13 @@ class Engine:
     def type_param(self, type_id: int, idx: int, value: int) -> None:
         _ck("gpu_actor_type_param",
             self.lib.gpu_actor_type_param(type_id, idx, int(value) & 0xFFFFFFFFFFFFFFFF))
+
+    def type_program(self, type_id: int, code) -> None:
+        """The behaviours of a GPU_ACTOR_HT_PROGRAM type (ponyc_amd.program
+        assembles them; include/gpu_actor.h has the instruction set)."""
+        c = np.ascontiguousarray(code, dtype=np.uint64)
+        _ck("gpu_actor_type_program",
+            self.lib.gpu_actor_type_program(type_id, c.ctypes.data, c.size))
 
     def type_reserve(self, type_id: int, n: int) -> None:
         """Room for n actors that behaviours spawn while running."""

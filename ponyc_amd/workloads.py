@@ -15,7 +15,8 @@ from .engine import (MSG_DTYPE, HT_RING, HT_PINGER, HT_PINGER_DET, HT_FANIN_SEND
                      HT_FANIN_ANALYZER, HT_GUPS_STREAMER, HT_GUPS_UPDATER, HT_STORM,
                      HT_FIFO_SRC, HT_FIFO_SINK, RING_SET, RING_PASS, PINGER_PING,
                      FANIN_SEND_MSGS, GUPS_APPLY, STORM_TOKEN, STORM_STORM, FIFO_BURST,
-                     HT_SPREADER, SPREADER_SPREAD)
+                     HT_SPREADER, SPREADER_SPREAD, HT_PROGRAM, NONE_ID)
+from . import program as P
 
 
 def _msgs(to, beh, arg) -> np.ndarray:
@@ -66,6 +67,49 @@ def ring(eng, size: int, count: int, passes: int, type_id: int = 0) -> dict:
 def ring_result(eng, w: dict) -> np.ndarray:
     """[recv, done] per actor (index = ring*size + id-1)."""
     return eng.state_read(w["type"])[2:4]
+
+
+def ring_prog(eng, size: int, count: int, passes: int, type_id: int = 0) -> dict:
+    """`ring` with the ring's behaviours as a program (GPU_ACTOR_HT_PROGRAM,
+    ponyc_amd.program.ring_program): the compiled table's constructor state
+    (engine.hip k_construct) written by the host, then the same sends."""
+    eng.type_register(type_id, 8, HT_PROGRAM)
+    eng.type_program(type_id, P.ring_program())
+    first = eng.create(type_id, size * count)
+    i = np.arange(size * count, dtype=np.uint64)
+    ring_i, pos = i // np.uint64(size), i % np.uint64(size)
+    st = np.zeros((8, size * count), dtype=np.uint64)
+    st[0] = np.where(pos == 0, np.uint64(NONE_ID),
+                     np.uint64(first) + ring_i * np.uint64(size) + (pos + np.uint64(1)) % np.uint64(size))
+    st[1] = pos + np.uint64(1)
+    eng.state_write(type_id, st)
+    heads = first + np.arange(count, dtype=np.uint64) * np.uint64(size)
+    m = np.empty(2 * count, dtype=MSG_DTYPE)
+    m[0::2] = _msgs(heads, RING_SET, heads + np.uint64(1 % size))
+    m[1::2] = _msgs(heads, RING_PASS, passes)
+    if passes == 0:
+        m = m[0::2]
+    _sendv(eng, m)
+    return {"type": type_id, "first": first, "n": size * count}
+
+
+def det_prog(eng, n: int, initial: int = 5, hops: int = 32, seed: int = 5489,
+             type_id: int = 0, batch: int = 0, mailbox_cap: int = 0) -> dict:
+    """`ubench(det=True)` with the ping as a program (ponyc_amd.program.det_program)."""
+    eng.type_register(type_id, 8, HT_PROGRAM)
+    if batch or mailbox_cap:
+        eng.type_config(type_id, batch, mailbox_cap)
+    eng.type_program(type_id, P.det_program(PINGER_PING))
+    eng.type_param(type_id, 0, n)
+    eng.type_param(type_id, 2, hops)
+    eng.type_param(type_id, 3, seed)
+    first = eng.create(type_id, n)
+    eng.type_param(type_id, 1, first)
+    i = np.arange(n, dtype=np.uint64)
+    parts = [_msgs(first + i, PINGER_PING, (i * np.uint64(initial) + np.uint64(k)) << np.uint64(32))
+             for k in range(initial)]
+    _sendv(eng, np.concatenate(parts) if parts else np.empty(0, dtype=MSG_DTYPE))
+    return {"type": type_id, "first": first, "n": n}
 
 
 # ---- examples/message-ubench -------------------------------------------------------

@@ -5,7 +5,7 @@ pinger — each run for a fixed number of busy supersteps (run_fixed: HIP
 events around the launches, gpu_actor_last_drain_ms), so the figure is the
 kernel's own, not the run loop's.
 
-    python scripts/profile_general.py [--stamps] [pinger det storm]
+    python scripts/profile_general.py [--stamps] [pinger det storm det_prog]
 
 --stamps loads libgpuactor_stamps.so and prints the median phase shares of
 the last step (zone_dev.h GPA_STAMP: 0 count | 1 scans | 2 place | 3 hot sort
@@ -33,6 +33,8 @@ CASES = {
     "pinger": (lambda e: W.ubench(e, M, 5, budget=1 << 40), 5 * M),
     "det": (lambda e: W.ubench(e, M, 5, det=True, hops=1000), 5 * M),
     "storm": (lambda e: W.storm(e, 8 * M, 4, 1000), 5 * 8 * M),
+    # C2-det's ping as a program (GPU_ACTOR_HT_PROGRAM, ponyc_amd.program)
+    "det_prog": (lambda e: W.det_prog(e, M, 5, hops=1000), 5 * M),
 }
 
 

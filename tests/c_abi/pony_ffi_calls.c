@@ -32,6 +32,7 @@ int32_t gpu_actor_type_register(uint32_t type_id, uint32_t state_words, uint32_t
 int32_t gpu_actor_type_config(uint32_t type_id, uint32_t batch, uint32_t mailbox_cap);
 int32_t gpu_actor_type_priority(uint32_t type_id, int32_t priority);
 int32_t gpu_actor_type_param(uint32_t type_id, uint32_t idx, uint64_t value);
+int32_t gpu_actor_type_program(uint32_t type_id, void* code, uint32_t n);
 int32_t gpu_actor_create(uint32_t type_id, uint64_t count, void* first);
 int32_t gpu_actor_type_reserve(uint32_t type_id, uint64_t n);
 int32_t gpu_actor_type_live(uint32_t type_id, void* live);
@@ -72,6 +73,7 @@ static int cpu_mode(void)
   EXPECT(gpu_actor_type_config(0, 100, 16), ESTATE);
   EXPECT(gpu_actor_type_priority(0, 1), ESTATE);
   EXPECT(gpu_actor_type_param(0, 0, 1), ESTATE);
+  EXPECT(gpu_actor_type_program(0, buf, 17), ESTATE);
   EXPECT(gpu_actor_create(0, 1, &u), ESTATE);
   EXPECT(gpu_actor_type_reserve(0, 1), ESTATE);
   EXPECT(gpu_actor_type_live(0, &u), ESTATE);
