@@ -29,6 +29,7 @@ template <int HT, int PM> constexpr step_kernel_t split_kernel()
   if constexpr(PM == 3 && !(HT >= 0 && two_pass<HT>()))
     return nullptr;
   else if constexpr(HT >= 0 && (two_pass<HT>() || HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM ||
+                                HT == GPU_ACTOR_HT_PROGRAM ||
                                 HT == kHtFifoPair))
     return k_step<HT, PM>;
   else return nullptr;

@@ -63,7 +63,7 @@ static_assert(kTile % kZoneThreads == 0 && kIdxCap % kZoneThreads == 0, "tile / 
 template <int HT> __host__ __device__ constexpr uint32_t small_regs()
 {
   return (HT == GPU_ACTOR_HT_PINGER || HT == GPU_ACTOR_HT_FANIN_SENDER ||
-          HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM) ? 16u : 8u;
+          HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM) ? 16u : HT == GPU_ACTOR_HT_PROGRAM ? 4u : 8u;
 }
 
 // A workgroup barrier that orders LDS only. __syncthreads() also waits for
