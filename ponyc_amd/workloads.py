@@ -82,6 +82,10 @@ def ring_prog(eng, size: int, count: int, passes: int, type_id: int = 0) -> dict
     st[0] = np.where(pos == 0, np.uint64(NONE_ID),
                      np.uint64(first) + ring_i * np.uint64(size) + (pos + np.uint64(1)) % np.uint64(size))
     st[1] = pos + np.uint64(1)
+    # each rank writes the actors it owns (id % n_ranks == rank), in id order
+    r = getattr(eng, "n_ranks", 1)
+    if r > 1:
+        st = st[:, ((np.uint64(first) + i) % np.uint64(r)) == np.uint64(eng.rank)]
     eng.state_write(type_id, st)
     heads = first + np.arange(count, dtype=np.uint64) * np.uint64(size)
     m = np.empty(2 * count, dtype=MSG_DTYPE)

@@ -62,6 +62,9 @@ CASES = {
     # ranks must still pick the same zone size (engine.hip relayout_zones)
     "zones_edge": (lambda e: W.ubench(e, 2 * 2048 * 638 + 1, 1, det=True, hops=3),
                    W.ubench_result, {}),
+    # behaviours as programs (GPU_ACTOR_HT_PROGRAM): sends across ranks
+    "ring_prog": (lambda e: W.ring_prog(e, 64, 4, 100), lambda e, w: e.state_read(w["type"]), {}),
+    "det_prog": (lambda e: W.det_prog(e, 3001, 3, hops=40), lambda e, w: e.state_read(w["type"]), {}),
 }
 
 

@@ -41,7 +41,7 @@ def test_host_plumbing_gloo(nproc):
 @pytest.mark.parametrize("case", ["ring", "ring1", "ubench", "ubench_det", "fanin", "gups",
                                   "storm", "fifo", "fifo_seq", "spreader", "mute", "priority",
                                   "spill", "spill_one_rank", "spill_one_rank_fixed", "xspill",
-                                  "xspill_det", "backlog", "zones_edge"])
+                                  "xspill_det", "backlog", "zones_edge", "ring_prog", "det_prog"])
 def test_two_ranks_one_gpu(case):
     out = _launch("mr_worker.py", 2, case)
     line = [l for l in out.splitlines() if l.startswith("MR_RESULT ")]
