@@ -276,6 +276,7 @@ struct HostType {
   uint64_t* d_state = nullptr;
   uint64_t* d_prog = nullptr;           // GPU_ACTOR_HT_PROGRAM: the behaviours' program
   uint32_t prog_n = 0;
+  bool prog_yields = false;             // it holds a YIELD: the small-step path leaves it
 };
 
 struct Engine {
@@ -506,6 +507,7 @@ int upload_types()
     memcpy(d.params, h.params, sizeof(d.params));
     d.prog = h.d_prog;
     d.prog_n = h.prog_n;
+    d.prog_pad = h.prog_yields ? 1u : 0u;
   }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_types), td, sizeof(td), 0,
     hipMemcpyHostToDevice, g.stream));
@@ -2035,6 +2037,9 @@ GPU_ACTOR_API int gpu_actor_type_program(uint32_t type_id, const uint64_t* code,
   }
   t.d_prog = d;
   t.prog_n = n;
+  t.prog_yields = false;
+  for(uint32_t k = GPU_ACTOR_PROG_ENTRIES; k < n; ++k)
+    t.prog_yields |= (code[k] & 0xFFu) == GPU_ACTOR_OP_YIELD;
   return t.created ? upload_types() : 0;
 }
 
@@ -2178,8 +2183,14 @@ bool sparse_ok()
 // limit). Returns its control block after the launch completes.
 int run_sparse(uint64_t max_steps, SparseCtl& out)
 {
-  hipLaunchKernelGGL(k_sparse, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
-    (unsigned long long)max_steps, g.d_ctl, g.sidx);
+  bool prog = false;
+  for(const HostType& t : g.types) prog |= t.created && t.ht == GPU_ACTOR_HT_PROGRAM;
+  if(prog)
+    hipLaunchKernelGGL(k_sparse<true>, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
+      (unsigned long long)max_steps, g.d_ctl, g.sidx);
+  else
+    hipLaunchKernelGGL(k_sparse<false>, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
+      (unsigned long long)max_steps, g.d_ctl, g.sidx);
   HIPCK(hipGetLastError());
   HIPCK(hipMemcpyAsync(g.h_ctl, g.d_ctl, sizeof(SparseCtl), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,

@@ -118,7 +118,7 @@ struct TypeDev {
   uint64_t* state;           // [words][lcount]
   uint64_t  params[GPU_ACTOR_MAX_PARAMS];
   const uint64_t* prog;      // GPU_ACTOR_HT_PROGRAM: the behaviours' program
-  uint32_t  prog_n, prog_pad;
+  uint32_t  prog_n, prog_pad;   // prog_pad bit 0: the program holds a YIELD
 };
 
 // One deferred carry copy: records rec(from + j), j < rem, of an actor's

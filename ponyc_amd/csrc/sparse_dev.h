@@ -125,6 +125,10 @@ __device__ __forceinline__ void sp_drain(const TypeDev& T, SparseCtx& a, const S
   for(int k = 0; k < NW; ++k) T.state[(size_t)k * T.lcount + a.li] = st[k];
 }
 
+// kProg: the engine holds program types (GPU_ACTOR_HT_PROGRAM); their
+// interpreter is compiled into a k_sparse of its own (in the one kernel it
+// cost the compiled ring 13 %: 41.2 -> 35.7 M msgs/s, profiles/r05p4_sparse_program_ab.txt)
+template <bool kProg>
 __device__ __forceinline__ void sp_dispatch(const TypeDev& Tref, SparseCtx& a, const SpList& S,
   uint32_t i, uint32_t g, uint32_t L)
 {
@@ -141,6 +145,9 @@ __device__ __forceinline__ void sp_dispatch(const TypeDev& Tref, SparseCtx& a, c
     SPCASE(GPU_ACTOR_HT_STORM)
     SPCASE(GPU_ACTOR_HT_FIFO_SRC)
     SPCASE(GPU_ACTOR_HT_FIFO_SINK)
+    case GPU_ACTOR_HT_PROGRAM:
+      if constexpr(kProg) sp_drain<GPU_ACTOR_HT_PROGRAM>(T, a, S, i, g);
+      break;
 #undef SPCASE
     default: break;
   }
@@ -172,6 +179,7 @@ __device__ __forceinline__ uint32_t sp_block_excl_scan(uint32_t v, uint32_t* s_t
 
 // Runs up to max_steps supersteps (0: no limit) starting from the records in
 // landing[cur]; R == 1 and no spawning types (the host checks).
+template <bool kProg>
 __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned long long max_steps,
   SparseCtl* ctl, uint32_t sidx)
 {
@@ -198,7 +206,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     s_tinfo[tid].lcount = T.lcount;
     s_tinfo[tid].batch = T.batch;
     // reducible types never run; spawning and yielding ones need the zone path
-    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER || T.ht == GPU_ACTOR_HT_PROGRAM ||
+    s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER ||
+                          (T.ht == GPU_ACTOR_HT_PROGRAM && (!kProg || (T.prog_pad & 1u))) ||
                           (T.ht == GPU_ACTOR_HT_FIFO_SINK && T.params[1] != 0)) ? kSpNoRun : 0u;
   }
   if(tid == 0) { sp_cnt[0] = 0; sp_cnt[1] = 0; s_over = 0; }
@@ -410,8 +419,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       // the usual case, one type for every run of the wave: its fields come
       // through scalar loads instead of a per-lane copy from constant memory
       const int tu = __builtin_amdgcn_readfirstlane(t);
-      if(__ballot(t != tu) == 0ull) sp_dispatch(c_types[tu], a, Sr, h_r, h_g, L);
-      else sp_dispatch(c_types[t], a, Sr, h_r, h_g, L);
+      if(__ballot(t != tu) == 0ull) sp_dispatch<kProg>(c_types[tu], a, Sr, h_r, h_g, L);
+      else sp_dispatch<kProg>(c_types[t], a, Sr, h_r, h_g, L);
       delivered += h_g;
       active += 1;
       sent += a.sent;
