@@ -489,6 +489,40 @@ bool defer_big_wanted()
 
 StepEntry pick_step_entry();
 
+// The hot-zone scratch words (hot_dev.h), in the order upload_types hands
+// them to the device; hot_bar_words() is the grid barrier's [0] arrivals, [1]
+// finished workgroups, [2] missed phases, [3] zones given back after a miss.
+inline size_t hot_words_before_bar()
+{
+  return 2 * (size_t)kMaxZones + (size_t)kMaxHot * kHotActors + (size_t)kMaxHot * 3 * kHotActors +
+         3 * (size_t)kHotBins + kHotActors;
+}
+inline uint32_t* hot_bar_words() { return g.d_hot + hot_words_before_bar(); }
+
+// k_hot's workgroups must all be resident at once (its phases meet at grid
+// barriers, hot_dev.h): kHotBlocks workgroups of kHotThreads with the LDS of
+// the larger zone geometry, against the occupancy the runtime reports for
+// this device (one workgroup per CU on half the CUs is what it needs; the
+// reported figure can exceed the hardware's by one workgroup per CU,
+// MI355X_MICROARCH.md, so one is taken off). Asked once per engine.
+bool hot_resident()
+{
+  static int cached = -1;
+  if(cached >= 0) return cached != 0;
+  int per_cu = 0, cus = 0;
+  const size_t lds = 5u * kHotActors * sizeof(uint32_t);
+  if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_hot),
+       (int)kHotThreads, lds) != hipSuccess ||
+     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g.device) != hipSuccess)
+  {
+    (void)hipGetLastError();
+    cached = 0;
+    return false;
+  }
+  cached = (uint64_t)std::max(per_cu - 1, per_cu > 0 ? 1 : 0) * (uint64_t)cus >= kHotBlocks ? 1 : 0;
+  return cached != 0;
+}
+
 int upload_types()
 {
   TypeDev td[GPU_ACTOR_MAX_TYPES];
@@ -560,10 +594,14 @@ int upload_types()
   g.defer_big = defer_big_wanted();
   // k_hot runs where backlogs build (the same engines as defer_big);
   // PONYC_AMD_HOT=0/1 forces it (tests, A/B)
+  // It runs only where its grid is resident at once (hot_resident): its
+  // phases meet at grid barriers.
   {
     const char* f = getenv("PONYC_AMD_HOT");
-    g.hot_on = pick_step_entry().hot && (f ? atoi(f) != 0 : g.defer_big);
+    g.hot_on = pick_step_entry().hot && (f ? atoi(f) != 0 : g.defer_big) && hot_resident();
     e.hot_on = g.hot_on ? 1u : 0u;
+    const char* t = getenv("PONYC_AMD_HOT_TEST");
+    e.hot_test = (t && atoi(t) != 0) ? 1u : 0u;
   }
   e.bigc = g.d_bigc; e.bigc_n = g.d_bigc_n; e.bigc_cap = kBigCopyCap;
   e.defer_big = g.defer_big ? 1u : 0u;
@@ -1776,8 +1814,7 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
   {
     // hot-zone scratch (hot_dev.h): prep, slot, counts, key ranges (fmin
     // starts at ~0), bins, bin counts, cursors, barrier
-    const size_t words = 2 * kMaxZones + kMaxHot * kHotActors + kMaxHot * 3 * kHotActors +
-                         3 * (size_t)kHotBins + kHotActors + 64;
+    const size_t words = hot_words_before_bar() + 64;
     HIPCK(hipMalloc(&g.d_hot, words * sizeof(uint32_t)));
     HIPCK(hipMemsetAsync(g.d_hot, 0, words * sizeof(uint32_t), g.stream));
     uint32_t* aux = g.d_hot + 2 * kMaxZones + kMaxHot * kHotActors;
@@ -2029,7 +2066,15 @@ GPU_ACTOR_API int gpu_actor_type_program(uint32_t type_id, const uint64_t* code,
   HostType& t = g.types[type_id];
   uint64_t* d = nullptr;
   HIPCK(hipMalloc(&d, (size_t)n * sizeof(uint64_t)));
-  HIPCK(hipMemcpy(d, code, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice));
+  // on the engine's stream like every other upload; the new buffer is freed
+  // if the copy fails
+  if(hipMemcpyAsync(d, code, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice, g.stream) !=
+       hipSuccess || hipStreamSynchronize(g.stream) != hipSuccess)
+  {
+    (void)hipGetLastError();
+    (void)hipFree(d);
+    return GPU_ACTOR_EHIP;
+  }
   if(t.d_prog)
   {
     HIPCK(hipStreamSynchronize(g.stream));          // no launch still reads the old one
@@ -2617,9 +2662,17 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
     HIPCK(hipMemcpyAsync(tn, g.d_trig_n, sizeof(tn), hipMemcpyDeviceToHost, g.stream));
     HIPCK(hipStreamSynchronize(g.stream));
   }
-  const uint64_t v[10] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
-                          g.n_zones, tn[0], tn[1], tn[2], g.zbits};
-  for(uint64_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
+  // + [10] hot zones k_hot gave back to k_step after a missed phase, [11]
+  // whether k_hot runs in this engine
+  uint32_t hb[4] = {0, 0, 0, 0};
+  if(g.d_hot)
+  {
+    HIPCK(hipMemcpyAsync(hb, hot_bar_words(), sizeof(hb), hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+  }
+  const uint64_t v[12] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+                          g.n_zones, tn[0], tn[1], tn[2], g.zbits, hb[3], g.hot_on ? 1u : 0u};
+  for(uint64_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
   return 0;
 }
 

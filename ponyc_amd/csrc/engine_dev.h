@@ -216,8 +216,12 @@ struct EngDev {
   // hot_prep[z] = step index + 1 of the step whose arrivals k_hot placed in
   // S, hot_slot[z] its slot; per slot the arrivals per actor (hot_cnt,
   // [kMaxHot][4096], cleared by k_step as it reads them) and key ranges
-  // (hot_aux); bins and cursors over the zone's big groups; the grid barrier
-  uint32_t hot_on, pad8;
+  // (hot_aux); bins and cursors over the zone's big groups; the grid
+  // barrier's words (hot_bar: [0] arrivals, [1] finished workgroups, [2]
+  // workgroups that missed a phase, [3] zones given back to k_step after such
+  // a miss). hot_test (PONYC_AMD_HOT_TEST=1, tests only): the last workgroup
+  // reports a missed phase for every hot zone, as a barrier timeout would.
+  uint32_t hot_on, hot_test;
   uint32_t* hot_prep;
   uint32_t* hot_slot;
   uint32_t* hot_cnt;
@@ -228,6 +232,10 @@ struct EngDev {
   uint32_t* hot_bar;
 };
 constexpr uint32_t kShards = 32;
+// landed records that make a zone hot (hot_dev.h). k_step consumes a prepared
+// zone's counts only on its scratch path, so a hot zone must never fit the
+// LDS index (zone_dev.h static_assert against kIdxCap).
+constexpr uint32_t kHotMin = 32768;
 
 
 __constant__ TypeDev c_types[GPU_ACTOR_MAX_TYPES];

@@ -7,7 +7,8 @@
 //
 // k_hot (kHotBlocks workgroups, launched right before k_step in engines that
 // build backlogs: EngDev::hot_on) finds the zones whose landing count is at
-// least kHotMin (every workgroup finds the same list), and for each, with a
+// least kHotMin and takes the kMaxHot of them with the lowest indices (every
+// workgroup the same list, by ballot in zone order), and for each, with a
 // grid barrier between phases:
 //   P1 count    each workgroup counts a slice of the landing buffer per actor
 //               in LDS (and the senders' id range and largest sequence number
@@ -23,8 +24,9 @@
 //               orders them);
 //   P4 sort     one thread per bin sorts its records by key in place (<= 16
 //               in registers), and the bins, counters and cursors are reset.
-// The zone is marked (hot_prep = step index + 1, its slot in hot_slot) and
-// k_step then takes its arrival counts from hot_cnt, finds the records where
+// The last workgroup to finish the zone marks it (hot_prep = step index + 1,
+// its slot in hot_slot) if every workgroup ran every phase (hot_zone_done),
+// and k_step then takes its arrival counts from hot_cnt, finds the records where
 // its scratch path would have placed them, and its big groups sorted.
 // Results are the same whichever workgroups did the work: records are placed
 // by cursor order only inside a bin or a small group, which are sorted (by
@@ -34,10 +36,9 @@
 
 namespace gpa {
 
-constexpr uint32_t kHotBlocks = 128;            // workgroups of k_hot (all resident)
+constexpr uint32_t kHotBlocks = 128;            // workgroups of k_hot (all resident: engine.hip hot_resident)
 constexpr uint32_t kHotThreads = 512;
-constexpr uint32_t kHotMin = 32768;             // landed records that make a zone hot
-constexpr uint32_t kMaxHot = 4;                 // hot zones prepared per step
+constexpr uint32_t kMaxHot = 4;                 // hot zones prepared per step (the lowest indices)
 constexpr uint32_t kHotBins = 1u << 20;         // bins over a zone's big groups
 constexpr uint32_t kHotBinItems = 8;            // records per bin aimed at
 constexpr uint32_t kHotMaxBins = 4096;          // bins per big group
@@ -49,6 +50,10 @@ constexpr uint32_t kHotActors = 4096;           // actors per zone (both geometr
 // (__syncthreads), lane 0's agent release with its own vmcnt wait (the
 // compiler may drop the one after buffer_wbl2), the counter add; then one
 // relaxed poll, an agent acquire (this CU's L1) and a barrier before any load.
+// Every spin is bounded: a workgroup that times out (never expected — the host
+// launches k_hot only when its grid is resident, engine.hip hot_resident)
+// goes on without the phases after it and reports the miss at the zone's end
+// (hot_zone_done), which then gives the zone back to k_step unprepared.
 __device__ __forceinline__ bool hot_barrier()
 {
   __shared__ uint32_t s_ok;
@@ -64,7 +69,7 @@ __device__ __forceinline__ bool hot_barrier()
     while((int32_t)(__hip_atomic_load(c_eng.hot_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
     {
       __builtin_amdgcn_s_sleep(2);
-      if(++spins > (1u << 26)) { s_ok = 0; break; }   // never expected: every workgroup is resident
+      if(++spins > (1u << 26)) { s_ok = 0; break; }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -90,6 +95,67 @@ __device__ __forceinline__ uint32_t* hot_aux(uint32_t slot, uint32_t k)
   return c_eng.hot_aux + ((size_t)slot * 3 + k) * kHotActors;
 }
 
+// The end of one hot zone, decided once for the whole grid by the last
+// workgroup to finish it (an arrival counter, never reset, like hot_bar's):
+// every workgroup first adds a miss to hot_bar[2] if it skipped a phase (its
+// `ok` is false), then arrives. The last arriver sees every report: the zone
+// is marked prepared only if it fits the bins (`fits`, the same in every
+// workgroup) and no workgroup missed a phase; otherwise its arrival counts
+// are cleared and k_step counts, places and sorts it itself from the landing
+// buffer, which k_hot only reads — the result is the same, only slower. A
+// miss is counted in hot_bar[3] (gpu_actor_debug_info).
+__device__ __forceinline__ void hot_zone_done(bool ok, bool fits, uint32_t z, uint32_t h,
+  uint32_t sidx, uint32_t za)
+{
+  __shared__ uint32_t s_clear;
+  uint32_t* const fin = c_eng.hot_bar + 1;
+  uint32_t* const bad = c_eng.hot_bar + 2;
+  __syncthreads();
+  if(threadIdx.x == 0)
+  {
+    if(!ok) __hip_atomic_fetch_add(bad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_clear = 0;
+    if((old % gridDim.x) == gridDim.x - 1u)
+    {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint32_t nbad = __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if(nbad)
+      {
+        __hip_atomic_store(bad, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(c_eng.hot_bar + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if(fits && nbad == 0u)
+      {
+        c_eng.hot_slot[z] = h;
+        c_eng.hot_prep[z] = sidx + 1u;
+      }
+      else
+        s_clear = nbad ? 2u : 1u;
+    }
+  }
+  __syncthreads();
+  if(s_clear)
+  {
+    uint32_t* const gcnt = c_eng.hot_cnt + (size_t)h * kHotActors;
+    for(uint32_t a = threadIdx.x; a < za; a += blockDim.x) gcnt[a] = 0;
+  }
+  if(s_clear == 2u)
+  {
+    // after a missed phase nothing is known about who cleared what: every
+    // bin, cursor and key range back to its resting value
+    for(uint32_t j = threadIdx.x; j < kHotBins; j += blockDim.x)
+    { c_eng.hot_hist[j] = 0; c_eng.hot_bcnt[j] = 0; c_eng.hot_cur[j] = 0; }
+    for(uint32_t a = threadIdx.x; a < kHotActors; a += blockDim.x)
+    {
+      c_eng.hot_cur[kHotBins + a] = 0;
+      hot_aux(h, 0)[a] = 0xFFFFFFFFu; hot_aux(h, 1)[a] = 0; hot_aux(h, 2)[a] = 0;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx)
 {
   extern __shared__ uint32_t s_h[];            // [5][za]
@@ -103,22 +169,33 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
                                               : (*c_eng.spill_flag != 0u);
   if(halt_now) return;                         // k_step will not run this step
   const uint32_t nz = c_eng.n_zones, za = 1u << c_eng.zbits;
+  // The hot zones with the kMaxHot lowest indices, in zone order — the same
+  // list in every workgroup (the others go to k_step's own path): each pass
+  // over kHotThreads zones ranks its hot ones by ballot, wave by wave.
   if(tid == 0) s_nlist = 0;
   __syncthreads();
-  for(uint32_t z = tid; z < nz; z += kHotThreads)
-    if(min(c_eng.land_n[cur][z], c_eng.zcapz[z]) >= kHotMin)
+  for(uint32_t z0 = 0; z0 < nz; z0 += kHotThreads)
+  {
+    const uint32_t z = z0 + tid;
+    const bool is_hot = z < nz && min(c_eng.land_n[cur][z], c_eng.zcapz[z]) >= kHotMin;
+    const unsigned long long m = __ballot(is_hot);
+    if(lane == 0) s_tmp[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t k = s_nlist, tot = s_nlist;
+    for(uint32_t w = 0; w < kHotThreads / 64; ++w)
     {
-      const uint32_t k = atomicAdd(&s_nlist, 1u);
-      if(k < kMaxHot) s_list[k] = z;
+      if(w < wv) k += s_tmp[w];
+      tot += s_tmp[w];
     }
-  __syncthreads();
+    k += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if(is_hot && k < kMaxHot) s_list[k] = z;
+    __syncthreads();
+    if(tid == 0) s_nlist = tot;
+    __syncthreads();
+    if(tot >= kMaxHot) break;                  // uniform
+  }
   const uint32_t nh = min(s_nlist, kMaxHot);
   if(nh == 0) return;                          // uniform over the grid
-  if(tid == 0)                                 // zone order: every workgroup alike
-    for(uint32_t i = 1; i < nh; ++i)
-      for(uint32_t j = i; j > 0 && s_list[j - 1] > s_list[j]; --j)
-      { const uint32_t t = s_list[j]; s_list[j] = s_list[j - 1]; s_list[j - 1] = t; }
-  __syncthreads();
   uint32_t* const s_cnt = s_h;                 // counts; then segment offsets
   uint32_t* const s_a = s_h + za;              // fmin; then bin bases
   uint32_t* const s_b = s_h + 2 * za;          // fmax; then bins per actor
@@ -220,11 +297,14 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
       __syncthreads();
     }
     const uint32_t nbins = s_bins;
-    if(nbins > kHotBins) ok = false;           // uniform: left to k_step's own path
+    // fits: uniform over the grid when every barrier held (each workgroup
+    // scanned the same counts); a zone past the bins is left to k_step's own
+    // path. `ok`: this workgroup ran every phase so far.
+    const bool fits = nbins <= kHotBins;
     uint32_t* const hist = c_eng.hot_hist;     // [nbins] records per bin -> (P2.5) bin starts
     uint32_t* const bcnt = c_eng.hot_bcnt;     // [nbins] records per bin (kept for P4)
     uint32_t* const bcur = c_eng.hot_cur;      // [nbins] cursors; [kHotBins + a] small groups
-    if(ok)
+    if(ok && fits)
       for(uint32_t i = c0 + tid; i < c1; i += kHotThreads)
       {
         const uint32_t w0 = Ld[i].w0;
@@ -239,7 +319,7 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
     ok = hot_barrier() && ok;
     HOT_RT(4);
     // ---- P2.5: each big group's bin starts (one workgroup per group)
-    if(ok)
+    if(ok && fits)
     {
       // this workgroup's actors a = bid + k G (a serial walk over every actor
       // with a division per step took 139 us)
@@ -287,8 +367,10 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
     HOT_RT(5);
     ok = hot_barrier() && ok;
     HOT_RT(6);
+    // (tests: the last workgroup misses P3 and P4, as after a barrier timeout)
+    if(c_eng.hot_test && bid == G - 1u) ok = false;
     // ---- P3: every record to its place in S
-    if(ok)
+    if(ok && fits)
       for(uint32_t i = c0 + tid; i < c1; i += kHotThreads)
       {
         const uint4 r = *reinterpret_cast<const uint4*>(Ld + i);
@@ -309,7 +391,7 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
     ok = hot_barrier() && ok;
     HOT_RT(8);
     // ---- P4: each bin sorted in place by key (distinct keys); counters reset
-    if(ok)
+    if(ok && fits)
       for(uint32_t j = bid * kHotThreads + tid; j < nbins; j += G * kHotThreads)
       {
         // the bin's actor: the last a with s_g[a] <= j (a small group after
@@ -367,26 +449,20 @@ __global__ void __launch_bounds__(kHotThreads) k_hot(uint32_t cur, uint32_t sidx
         }
         hist[j] = 0; bcnt[j] = 0; bcur[j] = 0;
       }
-    // per-actor scratch back to its resting values (hot_cnt stays: k_step
-    // reads it and clears it); bins never touched when !ok are zero already
+    else
+      // a zone given back to k_step: this workgroup's share of the bins
+      // cleared (a missed phase: the last workgroup clears them all below)
+      for(uint32_t j = bid * kHotThreads + tid; j < min(nbins, kHotBins); j += G * kHotThreads)
+      { hist[j] = 0; bcnt[j] = 0; bcur[j] = 0; }
+    // per-actor scratch back to its resting values (hot_cnt stays when the
+    // zone is prepared: k_step reads it and clears it)
     if(bid == 0)
       for(uint32_t a = tid; a < za; a += kHotThreads)
       {
         gfmin[a] = 0xFFFFFFFFu; gfmax[a] = 0; gsmax[a] = 0;
         bcur[kHotBins + a] = 0;
-        if(!ok) gcnt[a] = 0;
       }
-    if(!ok)
-    {
-      // give the zone back to k_step unprepared: its bin counts of P2 cleared
-      for(uint32_t j = bid * kHotThreads + tid; j < min(nbins, kHotBins); j += G * kHotThreads)
-      { hist[j] = 0; bcnt[j] = 0; bcur[j] = 0; }
-    }
-    else if(bid == 0 && tid == 0)
-    {
-      c_eng.hot_slot[z] = h;
-      c_eng.hot_prep[z] = sidx + 1u;
-    }
+    hot_zone_done(ok, fits, z, h, sidx, za);
     HOT_RT(9);
     // the next zone's P2 reuses the bins (after this one's P4 cleared them)
     if(h + 1 < nh) (void)hot_barrier();

@@ -56,6 +56,9 @@ constexpr uint32_t kTile = GPA_TILE;       // outbox records sorted per scatter 
 constexpr int kTilePer = kTile / kZoneThreads;  // tile records per thread
 constexpr int kIdxPer = kIdxCap / kZoneThreads; // landed records per thread on the LDS-index path
 static_assert(kTile % kZoneThreads == 0 && kIdxCap % kZoneThreads == 0, "tile / index split");
+// a zone k_hot prepared takes the scratch path, where k_step reads and clears
+// its hot_cnt slot: it must never fit the LDS index
+static_assert(kHotMin > kIdxCap, "hot zones take the scratch path");
 // Arrival groups up to this size are loaded at once and ordered in registers.
 // 16 where the handler does not read the message (pinger: the selection
 // compiles away) or the table's state is small; 8 elsewhere, to stay within

@@ -371,13 +371,13 @@ class Engine:
 
     def debug_info(self) -> dict:
         """Engine internals (diagnostic export, not in include/gpu_actor.h)."""
-        out = (ctypes.c_uint64 * 10)()
+        keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones",
+                "trig_n0", "trig_n1", "trig_n2", "zone_bits", "hot_missed", "hot_on"]
+        out = (ctypes.c_uint64 * len(keys))()
         fn = self.lib.gpu_actor_debug_info
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         fn.restype = ctypes.c_int
-        _ck("gpu_actor_debug_info", fn(out, 10))
-        keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones",
-                "trig_n0", "trig_n1", "trig_n2", "zone_bits"]
+        _ck("gpu_actor_debug_info", fn(out, len(keys)))
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
     def stream(self) -> int:

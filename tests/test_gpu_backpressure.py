@@ -130,3 +130,54 @@ def test_hot_group_sort_paths(engine_factory, oracle, monkeypatch, m, hot):
     monkeypatch.setenv("PONYC_AMD_HOT", hot)
     _both(engine_factory, oracle, lambda e: W.fifo(e, 3000, 1, 1, m, mailbox_cap=16),
           W.fifo_result)
+
+
+def _hot_zones_60_to_70(e):
+    """Idle ring actors fill zones 0-59 (type 0); 22,528 FIFO sinks fill zones
+    60-70 (type 1); 45,056 sources (type 2) burst 8 PUSHes each, so every
+    sink zone lands exactly kHotMin = 32,768 records in one step: eleven hot
+    zones, on both sides of the 64-zone wave boundary of k_hot's zone scan."""
+    from ponyc_amd.engine import HT_RING
+    e.type_register(0, 4, HT_RING)
+    e.create(0, 60 * 2048)
+    return W.fifo(e, 2 * 11 * 2048, 11 * 2048, 1, 8, sink_type=1, src_type=2, mailbox_cap=16)
+
+
+def test_hot_zones_past_kmaxhot(engine_factory, oracle, monkeypatch):
+    """More hot zones than k_hot prepares in a step (the list was
+    filled in the order the waves ran, so workgroups could disagree on it):
+    the kMaxHot lowest zone indices go to k_hot in every workgroup, the rest
+    to k_step's own path; bit-exact against the oracle."""
+    monkeypatch.setenv("PONYC_AMD_HOT", "1")
+    made = []
+
+    def factory(**kw):
+        e = engine_factory(**kw)
+        made.append(e)
+        return e
+    se, ce, _ = _both(factory, oracle, _hot_zones_60_to_70, W.fifo_result, mailbox_cap=16)
+    assert made[0].debug_info()["hot_on"] == 1
+    assert made[0].debug_info()["hot_missed"] == 0
+
+
+@pytest.mark.parametrize("shape", ["fanin_100k_4", "zones_60_70"])
+def test_hot_missed_phase_falls_back(engine_factory, oracle, monkeypatch, shape):
+    """A k_hot workgroup that misses a phase (forced here with
+    PONYC_AMD_HOT_TEST=1, as a grid-barrier timeout would) is reported at the
+    zone's end; the last workgroup then gives the zone back to k_step, which
+    counts, places and sorts it from the landing buffer: bit-exact, and the
+    misses are counted (gpu_actor_debug_info hot_missed)."""
+    monkeypatch.setenv("PONYC_AMD_HOT", "1")
+    monkeypatch.setenv("PONYC_AMD_HOT_TEST", "1")
+    made = []
+
+    def factory(**kw):
+        e = engine_factory(**kw)
+        made.append(e)
+        return e
+    setup = (_hot_zones_60_to_70 if shape == "zones_60_70"
+             else (lambda e: W.fifo(e, 100_000, 4, 2, 1, mailbox_cap=16)))
+    _both(factory, oracle, setup, W.fifo_result, mailbox_cap=16)
+    d = made[0].debug_info()
+    assert d["hot_on"] == 1
+    assert d["hot_missed"] > 0
