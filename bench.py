@@ -8,7 +8,8 @@ rand.int(N), as the reference's ping/send_pings do while `_go` is set). One
 "step" = one superstep: every pinger drains its mailbox and forwards each ping.
 
 Weak scaling: each rank owns 1,048,576 pingers of a global population of
-N x 1,048,576 (hash-partitioned, id % N); pings cross GPUs through the RCCL
+N x 1,048,576 (partitioned id % N: SURVEY §8 e1's alternative to the fmix32
+hash); pings cross GPUs through the RCCL
 exchange. value = delivered messages over all ranks / max-over-ranks time of
 the K timed steps.
 
@@ -489,7 +490,9 @@ def main():
                             f"{args.initial} initial pings, steady state",
                 "actors_per_gpu": args.actors, "actors_total": n_total,
                 "initial_pings": args.initial, "mailbox_cap": args.mailbox_cap, "batch": 100,
-                "parallelism": f"actor hash partition x{world} (id % {world})",
+                # SURVEY §8 e1's alternative partition (the north star's fmix32
+                # hash is not implemented): actor id -> rank id % N, local slot id / N
+                "parallelism": f"actor partition id % {world} over {world} rank(s)",
                 "exchange": exchange,
                 "ranks_share_gpu": bool(world > 1 and same_gpu()),
             },

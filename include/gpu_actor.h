@@ -30,7 +30,9 @@
 #define GPU_ACTOR_H
 
 #include <stdint.h>
+#ifndef __HIPCC_RTC__   /* (the run-time compiled step: engine.hip jit) */
 #include <stddef.h>
+#endif
 
 #if defined(__cplusplus)
 extern "C" {
@@ -369,6 +371,12 @@ GPU_ACTOR_API const char* gpu_actor_strerror(int code);
 #define GPU_ACTOR_OP_SEND   19  /* send behaviour (imm & 15), arg r[b], to r[a] */
 #define GPU_ACTOR_OP_MIX    20  /* r[d] = splitmix64 finaliser of r[a]        */
 #define GPU_ACTOR_OP_YIELD  21  /* end this actor's run after this behaviour  */
+#define GPU_ACTOR_OP_SPAWN  22  /* create an actor of type (imm & 0xFF) whose
+                                   constructor behaviour (imm >> 8 & 15) gets
+                                   arg r[b] (pony_create + its constructor
+                                   message, actor.c:688-734, gencall.c:606-612;
+                                   gpu_actor_type_reserve gives the room, past
+                                   it the spawn is dropped and counted)      */
 
 #define GPU_ACTOR_NONE 0xFFFFFFFFFFFFFFFFULL
 

@@ -438,7 +438,7 @@ static void run_program(const otype_t* t, uint64_t self, uint32_t beh, uint64_t 
     const uint32_t op = (uint32_t)(ins & 0xFF), d = (uint32_t)(ins >> 8) & 15;
     const uint64_t x = r[(ins >> 12) & 15], y = r[(ins >> 16) & 15];
     const int64_t imm = (int32_t)(uint32_t)(ins >> 32);
-    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_YIELD) break;
+    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_SPAWN) break;
     switch(op)
     {
       case GPU_ACTOR_OP_JZ:    if(x == 0) pc = (uint32_t)((int64_t)pc + imm); continue;
@@ -449,6 +449,12 @@ static void run_program(const otype_t* t, uint64_t self, uint32_t beh, uint64_t 
         else S.dropped++;
         continue;
       case GPU_ACTOR_OP_YIELD: S.yield_req = 1; continue;
+      case GPU_ACTOR_OP_SPAWN:
+        if(((uint32_t)imm & 0xFF) < GPU_ACTOR_MAX_TYPES)
+          spawn((uint32_t)imm & 0xFF, ((uint32_t)imm >> 8) & 15, y);
+        else
+          S.dropped++;
+        continue;
       case GPU_ACTOR_OP_LDI:   r[d] = (uint64_t)imm; break;
       case GPU_ACTOR_OP_LDP:   r[d] = t->params[imm & 7]; break;
       case GPU_ACTOR_OP_MOV:   r[d] = x; break;

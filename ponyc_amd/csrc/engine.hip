@@ -328,6 +328,11 @@ struct Engine {
   uint64_t host_seq = 0;
   uint64_t steps_total = 0;
   int sticky = 0;
+  // One rank: device work that can change the spill status or the counters
+  // bumps dev_epoch; a host read of either records the epoch it saw, so a
+  // read that nothing could have changed since is skipped (run_fixed's and
+  // gpu_actor_sync's host round trips, bench.py's timed region).
+  uint64_t dev_epoch = 1, sstat_epoch = 0, sticky_epoch = 0;
   hipError_t last_hip = hipSuccess;
   std::vector<hipEvent_t> ev;
   double last_drain_ms = 0.0;
@@ -655,6 +660,7 @@ int read_sstat()
   HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
     g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
+  g.sstat_epoch = g.dev_epoch;
   return 0;
 }
 
@@ -673,6 +679,7 @@ inline bool spill_pending()
 int fixup_spill()
 {
   const Engine::SpillStat st = *g.h_sstat;
+  g.dev_epoch++;
   if(R() == 1 && !st.spill_n[0] && !st.spill_n[1] && !st.halt) return 0;
   uint32_t n[2], most = 0;
   for(int p = 0; p < 2; ++p)
@@ -968,8 +975,15 @@ int pend_clear(uint32_t first, uint32_t n)
   return 0;
 }
 
+void sticky_from(const unsigned long long* st)
+{
+  if(st[ST_DROPPED] || st[ST_XCHG_OVERFLOW]) g.sticky = GPU_ACTOR_EMAILBOX;
+  else if(st[ST_SEQ_OVERFLOW]) g.sticky = GPU_ACTOR_ERANGE;
+}
+
 int check_sticky()
 {
+  if(R() == 1 && g.sticky_epoch == g.dev_epoch) return g.sticky;   // nothing ran since
   unsigned long long st[ST_COUNT];
   {
     const int rc = fold_counters(0, 0);
@@ -977,8 +991,8 @@ int check_sticky()
   }
   HIPCK(hipMemcpyAsync(st, g.d_stats, sizeof(st), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipStreamSynchronize(g.stream));
-  if(st[ST_DROPPED] || st[ST_XCHG_OVERFLOW]) g.sticky = GPU_ACTOR_EMAILBOX;
-  else if(st[ST_SEQ_OVERFLOW]) g.sticky = GPU_ACTOR_ERANGE;
+  g.sticky_epoch = g.dev_epoch;
+  sticky_from(st);
   return g.sticky;
 }
 
@@ -1520,6 +1534,7 @@ int spawn_process(uint32_t cur)
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
+  g.dev_epoch++;
   const StepEntry se = pick_step_entry();
   if(se.stub) return GPU_ACTOR_EINVAL;      // an experiment build without this table
   // bucket arrays (4 x buckets; six for an order-free zone's two passes:
@@ -1708,6 +1723,7 @@ inline bool host_msg_ok(const gpu_msg_t& m)
 int inject_locked(const gpu_msg_t* first, uint64_t n)
 {
   if(g.host_seq + n >= (1ull << 40)) return GPU_ACTOR_ERANGE;
+  g.dev_epoch++;
   if(n > g.d_msgs_cap)
   {
     if(g.d_msgs) HIPCK(hipFree(g.d_msgs));
@@ -2228,6 +2244,7 @@ bool sparse_ok()
 // limit). Returns its control block after the launch completes.
 int run_sparse(uint64_t max_steps, SparseCtl& out)
 {
+  g.dev_epoch++;
   bool prog = false;
   for(const HostType& t : g.types) prog |= t.created && t.ht == GPU_ACTOR_HT_PROGRAM;
   if(prog)
@@ -2272,6 +2289,8 @@ int settle_spills()
 {
   if(R() == 1)
   {
+    // (nothing ran since the last read: it stands)
+    if(g.sstat_epoch == g.dev_epoch) return spill_pending() ? fixup_spill() : 0;
     const int rc = read_sstat();
     if(rc) return rc;
     return spill_pending() ? fixup_spill() : 0;
@@ -2494,8 +2513,16 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
     bool any;
     if(R() == 1)
     {
+      // the spill status and the counters (for the sticky errors) in one
+      // host round trip
+      unsigned long long st[ST_COUNT];
+      rc = fold_counters(0, 0);
+      if(rc) return rc;
+      HIPCK(hipMemcpyAsync(st, g.d_stats, sizeof(st), hipMemcpyDeviceToHost, g.stream));
       rc = read_sstat();                    // synchronises the stream
       if(rc) return rc;
+      g.sticky_epoch = g.dev_epoch;
+      sticky_from(st);
       any = spill_pending();
     }
     else

@@ -15,8 +15,10 @@
 // A ZRec is {u32 seq<<16 | beh<<12 | to_local, u32 from, u64 arg}; its
 // canonical delivery key is (from << 16 | seq).
 #pragma once
+#ifndef __HIPCC_RTC__       // (also compiled at run time: engine.hip jit)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 #include "../../include/gpu_actor.h"
 #include "rng_dev.h"
 
@@ -347,6 +349,11 @@ struct ActorBase {
   uint32_t mute_to;      // the first such receiver
   uint32_t yield_req;    // the behaviour yielded (ponyint_actor_yield)
 
+  // kPlain: a context whose sends can neither run out of sequence numbers
+  // nor mute (the two-pass path: no backpressure anywhere, the zone's whole
+  // mail below seq_max) — send_serial then skips both checks
+  static constexpr bool kPlain = false;
+
   __device__ __forceinline__ void reset_common()
   {
     trig = nullptr; prev_o = 0; mute_hit = 0; mute_to = 0; yield_req = 0;
@@ -497,21 +504,23 @@ template <class A>
 __device__ __forceinline__ void send_serial(A& a, uint32_t to, uint32_t beh, uint64_t arg)
 {
   a.sent++;
-  if(a.seq >= c_eng.seq_max)
-  {
-    atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
-    return;
-  }
+  if constexpr(!A::kPlain)
+    if(a.seq >= c_eng.seq_max)
+    {
+      atomicAdd(&c_eng.stats[ST_SEQ_OVERFLOW], 1ull);
+      return;
+    }
   a.put(to, (a.seq << 16) | (beh << 12), arg);
   a.seq++;
   // ponyint_maybe_mute (actor.c:898-921): a send to an actor that is
   // overloaded or muted mutes a sender that is not overloaded itself, unless
   // it sends to itself; the sender stops after the behaviour it is running
-  if(a.trig && !a.prev_o && !a.mute_hit && to != a.self && a.trig[to] != 0)
-  {
-    a.mute_hit = 1;
-    a.mute_to = to;
-  }
+  if constexpr(!A::kPlain)
+    if(a.trig && !a.prev_o && !a.mute_hit && to != a.self && a.trig[to] != 0)
+    {
+      a.mute_hit = 1;
+      a.mute_to = to;
+    }
 }
 
 // ponyint_actor_yield (actor.c:675-679): end the actor's run after this
@@ -656,6 +665,10 @@ template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SRC>      { static constexpr int W
 template <> struct HT_Words<GPU_ACTOR_HT_FIFO_SINK>     { static constexpr int W = 11; };
 template <> struct HT_Words<GPU_ACTOR_HT_SPREADER>      { static constexpr int W = 5; };
 template <> struct HT_Words<GPU_ACTOR_HT_PROGRAM>       { static constexpr int W = 8; };
+// Behaviours as programs compiled at run time (engine.hip jit): the program
+// table's state, its handle() generated from the program words
+constexpr int kHtJit = 13;
+template <> struct HT_Words<kHtJit>                     { static constexpr int W = 8; };
 
 template <int HT> struct HtTag {};
 
@@ -834,7 +847,7 @@ __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_PROGRAM>, const TypeDe
     const uint32_t op = (uint32_t)ins & 0xFFu, d = ((uint32_t)ins >> 8) & 15u;
     const uint64_t x = r[((uint32_t)ins >> 12) & 15u], y = r[((uint32_t)ins >> 16) & 15u];
     const int64_t imm = (int32_t)(uint32_t)(ins >> 32);
-    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_YIELD) break;
+    if(op == GPU_ACTOR_OP_HALT || op > GPU_ACTOR_OP_SPAWN) break;
     if(op == GPU_ACTOR_OP_JZ || op == GPU_ACTOR_OP_JNZ || op == GPU_ACTOR_OP_JMP)
     {
       const bool take = op == GPU_ACTOR_OP_JMP || ((x == 0) == (op == GPU_ACTOR_OP_JZ));
@@ -850,6 +863,14 @@ __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_PROGRAM>, const TypeDe
       continue;
     }
     if(op == GPU_ACTOR_OP_YIELD) { actor_yield(a); continue; }
+    if(op == GPU_ACTOR_OP_SPAWN)
+    {
+      if(((uint32_t)imm & 0xFFu) < GPU_ACTOR_MAX_TYPES)
+        spawn_actor(a, (uint32_t)imm & 0xFFu, ((uint32_t)imm >> 8) & 15u, y);
+      else
+        atomicAdd(&c_eng.stats[ST_DROPPED], 1ull);
+      continue;
+    }
     uint64_t v;
     switch(op)
     {

@@ -2,8 +2,10 @@
 // from (packages/random: xoroshiro.pony:1-42, random.pony:143-193,
 // splitmix64.pony; PolyRand: examples/gups_basic/main.pony:167-216).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace gpa {
 

@@ -51,7 +51,8 @@ StepEntry GPA_STEP_ENTRY() { return { k_step_stub<GPA_STEP_HT>, step_upload, tru
                                       (uint32_t)kZoneThreads, kSortWork, 4u, false, nullptr, nullptr, nullptr }; }
 #else
 StepEntry GPA_STEP_ENTRY() { return { k_step<GPA_STEP_HT, 0>, step_upload, false, (uint32_t)kZoneBits,
-                                      (uint32_t)kZoneThreads, kSortWork, two_pass<GPA_STEP_HT>() ? 6u : 4u,
+                                      (uint32_t)kZoneThreads, kSortWork,
+                                      (two_pass<GPA_STEP_HT>() || dp_table<GPA_STEP_HT>()) ? 6u : 4u,
                                       GPA_STEP_HT < 0 || GPA_STEP_HT == kHtFifoPair,
                                       split_kernel<GPA_STEP_HT, 1>(), split_kernel<GPA_STEP_HT, 2>(),
                                       split_kernel<GPA_STEP_HT, 3>() }; }

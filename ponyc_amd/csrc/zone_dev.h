@@ -370,6 +370,31 @@ template <int HT> __host__ __device__ constexpr bool order_free()
   return HT == GPU_ACTOR_HT_PINGER;
 }
 
+// A table whose behaviours' sends depend on the message alone — target,
+// behaviour and argument a function of (receiver, behaviour, argument), never
+// of the state or of the order messages run in — and whose state updates
+// commute: message-ubench-det's ping and the storm (det_ping: count += 1,
+// acc ^= arg; the ring token to self + 1). Each behaviour sends at most one
+// message. Its plain zones run in two passes (k_step's `dp`): the sends are
+// counted per (drain round, bucket) while the landed records are counted, by
+// running each behaviour once on a throwaway state, in landing order; then
+// the zone drains straight into bucket-sorted LDS tiles — no outbox round
+// trip — and an actor's messages run in position order, each send stamped
+// with its message's canonical rank in the group (drain_commutative).
+template <int HT> __host__ __device__ constexpr bool msg_local()
+{
+  return HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM;
+}
+// ... on the 2048-actor geometry (the 4096-actor one's static LDS leaves no
+// room for the two more bucket arrays the counts take). GPA_DP=0: off (A/B).
+#ifndef GPA_DP
+#define GPA_DP 1
+#endif
+template <int HT> __host__ __device__ constexpr bool dp_table()
+{
+  return GPA_DP && HT >= 0 && msg_local<HT>() && kZoneBits == 11;
+}
+
 // A table set compiled as one k_step instantiation: the FIFO probe's source
 // and sink tables (the hot-receiver shape: sources fan in to order-sensitive
 // sinks). Its drain dispatches on the actor's table between these two only,
@@ -385,7 +410,7 @@ template <int HT> __host__ __device__ constexpr uint32_t seq_batch()
 
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
-  return HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_PROGRAM;
+  return HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_PROGRAM || HT == kHtJit;
 }
 
 // Drain one actor: handle up to min(batch, n) messages — carried mail, then
@@ -407,8 +432,8 @@ template <int HT> __host__ __device__ constexpr bool may_yield()
 //          order first, then in position order.
 // An order-free table (its behaviours ignore the message) handles a whole
 // group in position order: nothing is loaded for it.
-template <int HT, class Acc>
-__device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, Acc acc,
+template <int HT, class Acc, class Ctx>
+__device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, Ctx& a, Acc acc,
   uint32_t n, uint32_t nc, bool presorted)
 {
   // a register copy of the type's fields: read once, not re-read after every
@@ -601,6 +626,83 @@ __device__ __forceinline__ uint32_t drain_zone(const TypeDev& Tref, ZoneCtx& a, 
 }
 #undef GPA_RUN_SEQ
 
+// An actor of a message-local, commutative table (msg_local) whose whole
+// mail runs this step (no carried mail, no mute, no yield): the state ends
+// the same whatever order its messages run in, and so do the sends — except
+// their sequence numbers, which order them at their receivers. So the
+// messages run in position order, each send stamped with its message's rank
+// in the group by canonical key (the number of the group's keys below it):
+// ranks rise with the canonical order, so every receiver sorts these sends
+// exactly as it would sort seq 0, 1, 2, ... of a canonical drain (a message
+// sends at most one; the ranks' gaps, where a message sent nothing, order
+// nothing). Where drain_zone selects the smallest of 16 keys per message
+// (~140 VALU instructions: C2-det's drain was VALU-bound), a rank is 16
+// compares. A group past the register slots (<= kBigGroup in a plain zone;
+// ~15 of C2-det's 1M actors a step) must come in canonical order: it runs in
+// position order, each send stamped with its message's position.
+template <int HT, class Acc, class Ctx>
+__device__ __forceinline__ uint32_t drain_commutative(const TypeDev& Tref, Ctx& a, Acc acc, uint32_t g)
+{
+  constexpr uint32_t SM = small_regs<HT>();
+  const TypeDev T = Tref;
+  constexpr int NW = HT_Words<HT>::W;
+  uint64_t s[NW];
+#pragma unroll
+  for(int k = 0; k < NW; ++k) s[k] = T.state[(size_t)k * T.lcount + a.li];
+  uint64_t k[SM], v[SM];
+  auto load_slots = [&](uint32_t c0) __attribute__((always_inline)) {
+#pragma unroll
+    for(int j = 0; j < (int)SM; ++j)
+    {
+      if(c0 + j < g)
+      {
+        const ZRec r = acc.rec(c0 + j);
+        k[j] = (zkey(r) << 4) | ((r.w0 >> 12) & 0xFu); v[j] = r.arg;
+      }
+      else
+      {
+        k[j] = ~0ull; v[j] = 0;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): the loads, once
+  };
+  if(g <= SM)
+  {
+    // the whole group in the slots: each rank from the registers
+    load_slots(0u);
+#pragma unroll
+    for(int j = 0; j < (int)SM; ++j)
+      if((uint32_t)j < g)
+      {
+        uint32_t rank = 0;
+#pragma unroll
+        for(int i = 0; i < (int)SM; ++i) rank += k[i] < k[j] ? 1u : 0u;
+        a.seq = rank;
+        handle(HtTag<HT>{}, T, a, s, (uint32_t)k[j] & 0xFu, v[j]);
+      }
+  }
+  else
+    // a larger group is in canonical order already (the workgroup put it
+    // there: k_step's dp), so its position is its rank; four loads in flight
+    for(uint32_t p0 = 0; p0 < g; p0 += 4)
+    {
+      ZRec r[4];
+#pragma unroll
+      for(uint32_t u = 0; u < 4; ++u)
+        if(p0 + u < g) r[u] = acc.rec(p0 + u);
+#pragma unroll
+      for(uint32_t u = 0; u < 4; ++u)
+        if(p0 + u < g)
+        {
+          a.seq = p0 + u;
+          handle(HtTag<HT>{}, T, a, s, (r[u].w0 >> 12) & 0xFu, r[u].arg);
+        }
+    }
+#pragma unroll
+  for(int kk = 0; kk < NW; ++kk) T.state[(size_t)kk * T.lcount + a.li] = s[kk];
+  return g;
+}
+
 // The unhandled tail [done, n) of an actor's segment, already canonical, to
 // the next step's carry buffer at carry position co (positions past the
 // zone's capacity go to the spill list: never lost).
@@ -631,6 +733,7 @@ __device__ __forceinline__ void carry_out(Acc acc, uint32_t done, uint32_t n, ui
 // key << kPayBits | payload, the key compressed to (from - min from) << sbits
 // | seq, the payload the record's idx entry (or its position in S).
 constexpr uint32_t kBigGroup = 128;
+static_assert(kBigGroup < 256, "drain_commutative's 8-bit ranks");
 constexpr uint32_t kMaxBig = 32;            // big groups sorted per round of the loop
 constexpr uint32_t kPayBits = 20;           // payload bits of an item (group <= 2^20)
 static_assert(kPayBits == 20, "AccS::perm masks positions with 0xFFFFF");
@@ -1100,7 +1203,14 @@ __device__ __forceinline__ uint32_t emit_at(const uint4& r, uint32_t b, uint32_t
 
 // pass 1: count each send in its (round, bucket) — two rounds per u32 word,
 // 16 bits each (the zone's total is checked to fit)
+// (kPlain: the plan path runs only with no backpressure anywhere and the
+// zone's whole mail below seq_max; without the two checks in send_serial C2
+// runs 70.9-71.5 -> 69.6-70.1 us, profiles/r06c_plain_ctx_ab.txt)
+#ifndef GPA_PLAIN_CTX
+#define GPA_PLAIN_CTX 1
+#endif
 struct PlanCtx : ActorBase {
+  static constexpr bool kPlain = GPA_PLAIN_CTX;
   uint32_t* rh;
   uint32_t inc;
   __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg)
@@ -1112,24 +1222,140 @@ struct PlanCtx : ActorBase {
 // pass 2: the send's rank in its bucket comes from the round's cursor; the
 // tile holds it at start + rank; past the tile it goes straight to its chunk
 struct TileCtx : ActorBase {
+  static constexpr bool kPlain = GPA_PLAIN_CTX;
   uint4* tile;
   uint32_t* cur;          // [nb] bucket cursors in the tile, two rounds per word (half sh)
   const uint32_t* st;     // [nb] bucket starts in the tile, likewise
   const uint32_t* bs;     // [nb] the bucket chunk's next free place (chunk_dst word)
   uint32_t sh, inc;       // this round's half: shift, and 1 << shift
   uint32_t L0, nz, nxt, xover;
+  uint32_t tcap;          // records the tile holds
   __device__ __forceinline__ void put(uint32_t to, uint32_t w, uint64_t arg)
   {
     const uint32_t b = bucket_of(to);
     const uint32_t idx = (atomicAdd(&cur[b], inc) >> sh) & 0xFFFFu;
     uint4 r;
     r.x = to; r.y = w | src_local; r.z = (uint32_t)arg; r.w = (uint32_t)(arg >> 32);
-    if(idx < kPlanTile)
+    if(idx < tcap)
       tile[idx] = r;
     else
       xover += emit_at(r, b, bs[b], idx - ((st[b] >> sh) & 0xFFFFu), L0, nz, nxt);
   }
 };
+
+// The two-pass paths' shared steps (the pinger's plan path, and `dp` for the
+// message-local tables). Counts per (round, bucket) come packed two rounds
+// per u32 (16-bit halves): rh[0, nb) rounds 0-1, rh[nb, 2nb) rounds 2-3.
+// (1) one chunk per bucket for the zone's sends: bs[b] = chunk_dst word
+__device__ __forceinline__ uint32_t plan_reserve(const uint32_t* rh, uint32_t* bs, uint32_t nb,
+  uint32_t nz, uint32_t nxt, uint32_t tid)
+{
+  uint32_t n_atom = 0;
+  for(uint32_t b = tid; b < nb; b += kZoneThreads)
+  {
+    const uint32_t w0 = rh[b], w1 = rh[nb + b];
+    const uint32_t h = (w0 & 0xFFFFu) + (w0 >> 16) + (w1 & 0xFFFFu) + (w1 >> 16);
+    uint32_t base = 0;
+    if(h)
+    {
+      ++n_atom;
+      if(b < nz)
+        base = atomicAdd(&c_eng.land_n[nxt][b], h);
+      else
+        base = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
+    }
+    bs[b] = chunk_dst(b, base, h, nz);
+  }
+  return n_atom;
+}
+
+// (2) every round's bucket starts in the tile at once: exclusive scans of the
+// packed (round pair, bucket) counts, in place, each thread a contiguous run
+// of buckets; the cursors start at them. Three barriers for the four rounds
+// (a scan per round took three each). tot01 / tot23: the rounds' totals, packed.
+__device__ __forceinline__ void plan_scan(uint32_t* rh, uint32_t* cur, uint32_t nb, uint32_t* tmp2,
+  uint32_t tid, uint32_t& tot01, uint32_t& tot23)
+{
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
+  const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
+  uint32_t a = 0, c = 0;
+  for(uint32_t b = lo; b < hi; ++b) { a += rh[b]; c += rh[nb + b]; }
+  const uint32_t ia = wave_incl_scan(a, lane), ic = wave_incl_scan(c, lane);
+  if(lane == 63) { tmp2[wv] = ia; tmp2[kZoneWaves + wv] = ic; }
+  lds_sync();
+  if(wv < 2)
+  {
+    uint32_t* t = tmp2 + wv * kZoneWaves;
+    uint32_t x = lane < (uint32_t)kZoneWaves ? t[lane] : 0u;
+    x = wave_incl_scan(x, lane);
+    if(lane < (uint32_t)kZoneWaves) t[lane] = x;
+  }
+  lds_sync();
+  uint32_t ra = (wv ? tmp2[wv - 1] : 0u) + ia - a;
+  uint32_t rc = (wv ? tmp2[kZoneWaves + wv - 1] : 0u) + ic - c;
+  for(uint32_t b = lo; b < hi; ++b)
+  {
+    const uint32_t va = rh[b], vc = rh[nb + b];
+    rh[b] = ra; cur[b] = ra; ra += va;
+    rh[nb + b] = rc; cur[nb + b] = rc; rc += vc;
+  }
+  tot01 = tmp2[kZoneWaves - 1];
+  tot23 = tmp2[2 * kZoneWaves - 1];
+  lds_sync();
+}
+
+// (3) round r's tile (m records, sorted by bucket) to the chunks: runs of one
+// chunk per wave store, every record of the thread read before the first
+// store; then each chunk's next free place for the next round (the other
+// half of bs: this round's emit still reads this one) = + the round's count
+// of the bucket, the difference of consecutive starts. Returns the records
+// the exchange lost (emit_rec).
+__device__ __forceinline__ uint32_t plan_emit(const uint4* tile, uint32_t m, const uint32_t* rst,
+  const uint32_t* bsr, uint32_t* bsw, uint32_t sh, uint32_t tr, uint32_t nb, uint32_t L0,
+  uint32_t nz, uint32_t nxt, uint32_t tid)
+{
+  uint32_t xover = 0;
+  constexpr uint32_t kEU = GPA_EMIT_UNROLL;
+  for(uint32_t q0 = 0; q0 < m; q0 += kEU * kZoneThreads)
+  {
+    uint4 rec[kEU];
+#pragma unroll
+    for(uint32_t u = 0; u < kEU; ++u)
+    {
+      const uint32_t q = q0 + u * kZoneThreads + tid;
+      if(q < m) rec[u] = tile[q];
+    }
+#pragma unroll
+    for(uint32_t u = 0; u < kEU; ++u)
+    {
+      const uint32_t q = q0 + u * kZoneThreads + tid;
+      if(q < m)
+      {
+        const uint32_t b = bucket_of(rec[u].x);
+        xover += emit_at(rec[u], b, bsr[b], q - ((rst[b] >> sh) & 0xFFFFu), L0, nz, nxt);
+      }
+    }
+  }
+  for(uint32_t b = tid; b < nb; b += kZoneThreads)
+  {
+    const uint32_t s0 = (rst[b] >> sh) & 0xFFFFu;
+    const uint32_t s1 = b + 1 < nb ? (rst[b + 1] >> sh) & 0xFFFFu : tr;
+    bsw[b] = bsr[b] + (s1 - s0);
+  }
+  return xover;
+}
+
+// dp: the zone's LDS index at the end of the pool (nl entries, the start
+// 16-B aligned), and the tile before it
+__device__ __forceinline__ uint16_t* dp_index(uint4* pool, uint32_t nl)
+{
+  return reinterpret_cast<uint16_t*>(pool + kTile) - ((nl + 7u) & ~7u);
+}
+__device__ __forceinline__ uint32_t dp_tile_cap(uint32_t nl)
+{
+  return (uint32_t)(kTile * sizeof(uint4) - ((nl + 7u) & ~7u) * sizeof(uint16_t)) / (uint32_t)sizeof(uint4);
+}
 
 // 2 workgroups of kZoneThreads per CU: minimum waves per SIMD = 2 * 512 / 256 = 4
 // HTS >= 0: every serial actor of this engine runs handler table HTS (the host
@@ -1225,6 +1451,10 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
   // hot-group sort and the mute checks, which then need no registers
   constexpr bool kPlanSplit = HTS >= 0 && two_pass<HTS>();
   constexpr bool kSimple = PM == 1 && !kPlanSplit;
+  // ... of a message-local table, plain zones whose actors all drain whole
+  // this step run in two passes (dp, below)
+  constexpr bool kDP = kSimple && dp_table<HTS>();
+  bool dp = false;
   // (the mark is the step's index + 1: nothing clears it, and a step that
   // halted — and runs again with the same index — marked no zone)
   if constexpr(PM == 2)
@@ -1298,7 +1528,7 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
   uint8_t* const tb_out = c_eng.trig_own[nxt];
 
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) { s_cnt[i] = 0; s_ccnt[i] = 0; }
-  for(uint32_t b = tid; b < nb; b += kZoneThreads) s_hist[b] = 0;
+  for(uint32_t b = tid; b < (kDP ? 2u : 1u) * nb; b += kZoneThreads) s_hist[b] = 0;
   if(tid == 0) { s_nout = 0; s_ntrig = 0; s_nmix = 0; s_tot = 0; }
   __syncthreads();
   GPA_STAMP(0);
@@ -1413,7 +1643,51 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
       }
     }
   uint32_t wr[kIdxPer];
-  if(use_idx)
+  if constexpr(kDP)
+  {
+    // dp's first pass rides on the count: each landed record, whole (its
+    // line is read for the count anyway), in chunks of kDpChunk per thread;
+    // its behaviour runs on a throwaway state with a counting context, whose
+    // send is counted in the receiving actor's drain round and its bucket
+    // (the sends of a message-local behaviour do not depend on the state or
+    // the order: the second pass, in canonical order, makes the same ones)
+    constexpr int kDpChunk = 8;
+    static_assert(kIdxPer % kDpChunk == 0, "dp count chunks");
+    const TypeDev& T = c_types[tz];
+    PlanCtx pc;
+    pc.reset_common();
+    pc.type = tz;
+#pragma unroll
+    for(int u0 = 0; u0 < kIdxPer; u0 += kDpChunk)
+    {
+      uint4 rr[kDpChunk];
+#pragma unroll
+      for(int v = 0; v < kDpChunk; ++v)
+      {
+        const uint32_t i = (u0 + v) * kZoneThreads + tid;
+        if(i < nl) rr[v] = ld16(reinterpret_cast<const uint4*>(Ld + i));
+        else rr[v].x = 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for(int v = 0; v < kDpChunk; ++v)
+      {
+        wr[u0 + v] = rr[v].x;
+        if(rr[v].x == 0xFFFFFFFFu) continue;
+        const uint32_t act = rr[v].x & kZoneMask;
+        wr[u0 + v] = (atomicAdd(&s_cnt[act], 1u) << kZoneBits) | act;
+        const uint32_t rd = act / kZoneThreads;               // its drain round
+        pc.rh = s_hist + (rd >> 1) * nb;
+        pc.inc = (rd & 1u) ? 0x10000u : 1u;
+        pc.self = (L0 + act) * R + me;
+        pc.li = L0 + act - T.lfirst;
+        pc.src_local = act;
+        uint64_t junk[HT_Words<HTS>::W] = {};
+        handle(HtTag<HTS>{}, T, pc, junk, (rr[v].x >> 12) & 0xFu,
+               ((uint64_t)rr[v].w << 32) | rr[v].z);
+      }
+    }
+  }
+  else if(use_idx)
   {
 #pragma unroll
     for(int u = 0; u < kIdxPer; ++u)
@@ -1518,6 +1792,35 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
       int big = 0;
       for(uint32_t i = tid; i < kZone; i += kZoneThreads) big |= s_cnt[i] > kBigGroup;
       if(__syncthreads_or(big)) return false;         // a hot group: left to PM 2
+      if constexpr(kDP)
+      {
+        // two passes when every actor's mail runs this step (its batch holds
+        // it: nothing carries over, which the first pass could not know)
+        // Groups past drain_commutative's register slots are put in
+        // canonical order by the workgroup first (listed here, at most
+        // kMaxStage of them with kZoneThreads records in all: else PM 2).
+        const uint32_t bt = c_types[tz].prio ? 0xFFFFFFFFu : c_types[tz].batch;
+        if(tid == 0) { s_stn = 0; s_sto[0] = 0; }
+        __syncthreads();
+        int over = 0;
+        for(uint32_t i = tid; i < kZone; i += kZoneThreads)
+        {
+          const uint32_t c = s_cnt[i];
+          over |= c > bt;
+          if(c > small_regs<HTS>())
+          {
+            const uint32_t k = atomicAdd(&s_stn, 1u);
+            if(k < kMaxStage) s_stl[k] = i;
+            atomicAdd(&s_sto[0], c);
+          }
+        }
+        __syncthreads();
+        over |= s_stn > kMaxStage || s_sto[0] > (uint32_t)kZoneThreads;
+        dp = !__syncthreads_or(over);
+        // (otherwise left to PM 2's general path: PM 1 has written nothing
+        // outside LDS, and keeps only the two-pass drain's registers)
+        if(!dp) return false;
+      }
     }
     take_mail();
   }
@@ -1562,13 +1865,16 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
   // (S path: carried mail stays where it is, read in place through AccS)
   if(use_idx)
   {
-    // LDS index only: records stay in the landing buffer
+    // LDS index only: records stay in the landing buffer (dp: at the pool's
+    // end, so that the rest of the pool is one tile once the per-actor arrays
+    // are in registers)
+    uint16_t* const s_ix = dp ? dp_index(s_pool, nl) : s_idx;
 #pragma unroll
     for(int u = 0; u < kIdxPer; ++u)
       if(wr[u] != 0xFFFFFFFFu)
       {
         const uint32_t act = wr[u] & kZoneMask;
-        s_idx[s_off[act] + s_ccnt[act] + (wr[u] >> kZoneBits)] = (uint16_t)(nc + u * kZoneThreads + tid);
+        s_ix[s_off[act] + s_ccnt[act] + (wr[u] >> kZoneBits)] = (uint16_t)(nc + u * kZoneThreads + tid);
       }
   }
   else
@@ -1778,58 +2084,14 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
       lds_sync();
       GPA_STAMP(3);
       // one chunk per bucket for the zone's sends
-      for(uint32_t b = tid; b < nb; b += kZoneThreads)
-      {
-        const uint32_t w0 = s_rh[b], w1 = s_rh[nb + b];
-        const uint32_t h = (w0 & 0xFFFFu) + (w0 >> 16) + (w1 & 0xFFFFu) + (w1 >> 16);
-        uint32_t base = 0;
-        if(h)
-        {
-          ++n_atom;
-          if(b < nz)
-            base = atomicAdd(&c_eng.land_n[nxt][b], h);
-          else
-            base = (uint32_t)atomicAdd(&c_eng.xcount[b - nz], (unsigned long long)h);
-        }
-        s_bs[b] = chunk_dst(b, base, h, nz);
-      }
+      n_atom += plan_reserve(s_rh, s_bs, nb, nz, nxt, tid);
       GPA_STAMP(5);
 #ifdef GPA_STAMPS
       const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
 #endif
-      // every round's bucket starts in the tile at once: exclusive scans of
-      // the packed (round pair, bucket) counts, in place, each thread a
-      // contiguous run of buckets; the cursors start at them. Three barriers
-      // for the four rounds (a scan per round took three each).
+      // every round's bucket starts in the tile at once
       uint32_t tot01, tot23;
-      {
-        const uint32_t per = (nb + kZoneThreads - 1) / kZoneThreads;
-        const uint32_t lo = min(tid * per, nb), hi = min(lo + per, nb);
-        uint32_t a = 0, c = 0;
-        for(uint32_t b = lo; b < hi; ++b) { a += s_rh[b]; c += s_rh[nb + b]; }
-        const uint32_t ia = wave_incl_scan(a, lane), ic = wave_incl_scan(c, lane);
-        if(lane == 63) { s_tmp2[wv] = ia; s_tmp2[kZoneWaves + wv] = ic; }
-        lds_sync();
-        if(wv < 2)
-        {
-          uint32_t* t = s_tmp2 + wv * kZoneWaves;
-          uint32_t x = lane < (uint32_t)kZoneWaves ? t[lane] : 0u;
-          x = wave_incl_scan(x, lane);
-          if(lane < (uint32_t)kZoneWaves) t[lane] = x;
-        }
-        lds_sync();
-        uint32_t ra = (wv ? s_tmp2[wv - 1] : 0u) + ia - a;
-        uint32_t rc = (wv ? s_tmp2[kZoneWaves + wv - 1] : 0u) + ic - c;
-        for(uint32_t b = lo; b < hi; ++b)
-        {
-          const uint32_t va = s_rh[b], vc = s_rh[nb + b];
-          s_rh[b] = ra; s_cur[b] = ra; ra += va;
-          s_rh[nb + b] = rc; s_cur[nb + b] = rc; rc += vc;
-        }
-        tot01 = s_tmp2[kZoneWaves - 1];
-        tot23 = s_tmp2[2 * kZoneWaves - 1];
-        lds_sync();
-      }
+      plan_scan(s_rh, s_cur, nb, s_tmp2, tid, tot01, tot23);
 #ifdef GPA_STAMPS
       GPA_ACC(9, t_scan);
 #endif
@@ -1837,6 +2099,7 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
       TileCtx tc;
       tc.reset_common();
       tc.tile = tile;
+      tc.tcap = kPlanTile;
       tc.L0 = L0; tc.nz = nz; tc.nxt = nxt; tc.xover = 0;
       uint32_t dz = 0;
 #ifdef GPA_STAMPS
@@ -1880,41 +2143,9 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
         GPA_ACC(10, t_hand);
         t_emit = __builtin_amdgcn_s_memtime();
 #endif
-        // the tile, sorted by bucket, to the chunks: runs of one chunk per wave
-        // store; every record of the thread read before the first store
-        {
-          const uint32_t m = min(tr, kPlanTile);
-          constexpr uint32_t kEU = GPA_EMIT_UNROLL;
-          for(uint32_t q0 = 0; q0 < m; q0 += kEU * kZoneThreads)
-          {
-            uint4 rec[kEU];
-#pragma unroll
-            for(uint32_t u = 0; u < kEU; ++u)
-            {
-              const uint32_t q = q0 + u * kZoneThreads + tid;
-              if(q < m) rec[u] = tile[q];
-            }
-#pragma unroll
-            for(uint32_t u = 0; u < kEU; ++u)
-            {
-              const uint32_t q = q0 + u * kZoneThreads + tid;
-              if(q < m)
-              {
-                const uint32_t b = bucket_of(rec[u].x);
-                xover += emit_at(rec[u], b, bsr[b], q - ((rst[b] >> sh) & 0xFFFFu), L0, nz, nxt);
-              }
-            }
-          }
-        }
-        // the chunks' next free places, for the next round (the other half:
-        // this round's emit still reads this one): + the round's count of the
-        // bucket, the difference of consecutive starts
-        for(uint32_t b = tid; b < nb; b += kZoneThreads)
-        {
-          const uint32_t s0 = (rst[b] >> sh) & 0xFFFFu;
-          const uint32_t s1 = b + 1 < nb ? (rst[b + 1] >> sh) & 0xFFFFu : tr;
-          bsw[b] = bsr[b] + (s1 - s0);
-        }
+        // the tile, sorted by bucket, to the chunks; the chunks' next free
+        // places for the next round
+        xover += plan_emit(tile, min(tr, kPlanTile), rst, bsr, bsw, sh, tr, nb, L0, nz, nxt, tid);
         lds_sync();
 #ifdef GPA_STAMPS
         emit_clk += __builtin_amdgcn_s_memtime() - t_emit;
@@ -1944,7 +2175,132 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
       xover += tc.xover;
       if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
     }
-  if(!(PM == 1 && kPlanSplit) && !plan)
+  if constexpr(kDP)
+    if(dp)
+    {
+      // ---- 3''. message-local plain zone, second pass: the canonical drain
+      //      straight into bucket-sorted LDS tiles, one per drain round -------
+      const TypeDev& T = c_types[tz];
+      {
+        // the listed groups (past the register slots) into canonical order in
+        // the index: one thread per record counts the group's keys below its
+        // own, then every record moves to its rank (keys are distinct)
+        uint16_t* const s_ix = dp_index(s_pool, nl);
+        const uint32_t nbg = s_stn;                        // <= kMaxStage (dp)
+        if(nbg)
+        {
+          if(tid == 0)
+          {
+            uint32_t o = 0;
+            for(uint32_t k = 0; k < nbg; ++k) { s_sto[k] = o; o += s_cnt[s_stl[k]]; }
+            s_sto[nbg] = o;                                  // <= kZoneThreads (dp)
+          }
+          lds_sync();
+          uint16_t x = 0;
+          uint32_t rank = 0, off = 0;
+          if(tid < s_sto[nbg])
+          {
+            uint32_t k = 0;
+            while(k + 1 < nbg && s_sto[k + 1] <= tid) ++k;
+            const uint32_t i = s_stl[k], g = s_cnt[i];
+            off = s_off[i];
+            x = s_ix[off + tid - s_sto[k]];
+            const uint64_t key = zkey(ld_rec(Ld + x));
+            for(uint32_t j0 = 0; j0 < g; j0 += 4)
+            {
+              uint64_t kk[4];
+#pragma unroll
+              for(uint32_t u = 0; u < 4; ++u)
+                kk[u] = j0 + u < g ? zkey(ld_rec(Ld + s_ix[off + j0 + u])) : ~0ull;
+#pragma unroll
+              for(uint32_t u = 0; u < 4; ++u) rank += kk[u] < key ? 1u : 0u;
+            }
+          }
+          __syncthreads();
+          if(tid < s_sto[nbg]) s_ix[off + rank] = x;
+          __syncthreads();
+        }
+      }
+      uint32_t* const s_rh = s_dyn;             // [2][nb] sends per (round, bucket) -> tile starts
+      uint32_t* const s_cur = s_dyn + 2 * nb;   // [2][nb] tile cursors
+      uint32_t* const s_bs = s_dyn + 4 * nb;    // [2][nb] chunks' next free places (ping-pong)
+      n_atom += plan_reserve(s_rh, s_bs, nb, nz, nxt, tid);
+      uint32_t tot01, tot23;
+      plan_scan(s_rh, s_cur, nb, s_tmp2, tid, tot01, tot23);
+      // each thread's actors (one a round) in registers: the per-actor arrays'
+      // part of the pool becomes the tile, up to the index at its end
+      // (packed: segment offset << 8 | count; plain zones' counts are at
+      // most kBigGroup, their offsets below kIdxCap)
+      static_assert(kBigGroup < 256 && kIdxCap <= (1u << 24), "dn / doff pack");
+      uint32_t dno[kRounds];
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        const uint32_t i = r * kZoneThreads + tid;
+        dno[r] = i < nact ? (s_off[i] << 8) | s_cnt[i] : 0u;
+      }
+      lds_sync();
+      GPA_STAMP(8);                           // diagnostic build: the rounds start
+#ifdef GPA_STAMPS
+      if(tid == 0) { c_eng.dbg[z * kDbgSlots + 9] = 0; c_eng.dbg[z * kDbgSlots + 10] = 0; }
+#endif
+      const uint16_t* const s_ix = dp_index(s_pool, nl);
+      TileCtx tc;
+      tc.reset_common();
+      tc.tile = s_pool;
+      tc.tcap = dp_tile_cap(nl);
+      tc.L0 = L0; tc.nz = nz; tc.nxt = nxt; tc.xover = 0;
+      tc.type = tz;
+      uint32_t dz = 0;
+#pragma unroll
+      for(uint32_t r = 0; r < kRounds; ++r)
+      {
+        const uint32_t sh = (r & 1u) * 16u;
+        const uint32_t* const rst = s_rh + (r >> 1) * nb;
+        const uint32_t tr = (((r >> 1) ? tot23 : tot01) >> sh) & 0xFFFFu;
+        tc.cur = s_cur + (r >> 1) * nb;
+        const uint32_t* const bsr = s_bs + (r & 1u) * nb;
+        uint32_t* const bsw = s_bs + ((r & 1u) ^ 1u) * nb;
+        tc.st = rst; tc.bs = bsr;
+        tc.sh = sh; tc.inc = 1u << sh;
+#ifdef GPA_STAMPS
+        const unsigned long long t_dr = __builtin_amdgcn_s_memtime();
+#endif
+        if(dno[r] & 0xFFu)
+        {
+          const uint32_t i = r * kZoneThreads + tid;
+          const uint32_t L = L0 + i;
+          tc.li = L - T.lfirst;
+          tc.self = L * R + me;
+          tc.src_local = i;
+          tc.seq = 0;
+          const uint32_t d = drain_commutative<HTS>(T, tc,
+            AccIdx{const_cast<uint16_t*>(s_ix) + (dno[r] >> 8), C, Ld, 0u}, dno[r] & 0xFFu);
+          // overloaded iff a full batch ran (batch_limit_reached,
+          // actor.c:369-381); nothing here mutes
+          const bool full = T.prio ? (d % T.batch == 0u) : d == T.batch;
+          s_tb[i] = full ? 1u : 0u;
+          if(full) atomicAdd(&s_ntrig, 1u);
+          delivered += d;
+          active += 1;
+          dz += d;
+        }
+        lds_sync();
+#ifdef GPA_STAMPS
+        GPA_ACC(9, t_dr);                     // the round's drain (to its barrier)
+        const unsigned long long t_em = __builtin_amdgcn_s_memtime();
+#endif
+        xover += plan_emit(s_pool, min(tr, tc.tcap), rst, bsr, bsw, sh, tr, nb, L0, nz, nxt, tid);
+        lds_sync();
+#ifdef GPA_STAMPS
+        GPA_ACC(10, t_em);                    // the round's tile emit
+#endif
+      }
+      sent = tc.sent;
+      xover += tc.xover;
+      if(dz) atomicAdd(&s_bytype[tz], (unsigned long long)dz);
+    }
+  if(!(PM == 1 && kPlanSplit) && !plan && !dp)
   {
   // s_aux will hold each actor's unhandled remainder (known after it ran)
   for(uint32_t i = tid; i < kZone; i += kZoneThreads) s_aux[i] = 0;
@@ -2273,7 +2629,7 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
     }
 
   // ---- 4. one chunk per destination bucket ----------------------------------------
-  if(!(PM == 1 && kPlanSplit) && !plan)
+  if(!(PM == 1 && kPlanSplit) && !plan && !dp)
   {
   uint32_t* s_tcnt = s_dyn + 2 * nb;    // records of the tile per bucket
   uint32_t* s_tst = s_dyn + 3 * nb;     // bucket start within the sorted tile

@@ -20,7 +20,7 @@ ENTRIES = 16
 MAX_STEPS = 4096
 OPS = {"halt": 0, "ldi": 1, "ldp": 2, "mov": 3, "add": 4, "sub": 5, "mul": 6, "mulhi": 7,
        "and": 8, "or": 9, "xor": 10, "shl": 11, "shr": 12, "addi": 13, "ltu": 14, "eq": 15,
-       "jz": 16, "jnz": 17, "jmp": 18, "send": 19, "mix": 20, "yield": 21}
+       "jz": 16, "jnz": 17, "jmp": 18, "send": 19, "mix": 20, "yield": 21, "spawn": 22}
 R_ARG, R_SELF, R_BEH = 8, 9, 10
 
 
@@ -74,6 +74,12 @@ class Program:
     def jnz(self, a, label): self._jump("jnz", a, label)
     def jmp(self, label): self._jump("jmp", 0, label)
     def send(self, to, beh, arg): self._op("send", 0, to, arg, imm=beh)
+    def spawn(self, type_id, beh, arg):
+        """pony_create of an actor of type `type_id` + its constructor message
+        (behaviour `beh`, argument r[arg]); its id is assigned when the step ends."""
+        if not (0 <= type_id < 256 and 0 <= beh < 16):
+            raise ValueError("spawn type < 256, behaviour < 16")
+        self._op("spawn", 0, 0, arg, imm=type_id | beh << 8)
     def yield_(self): self._op("yield")
     def halt(self): self._op("halt")
     def raw(self, w: int) -> None:
@@ -143,5 +149,60 @@ def det_program(beh: int = 0) -> np.ndarray:
     p.or_(15, 15, 13)
     p.send(14, beh, 15)
     p.label("end")
+    p.halt()
+    return p.assemble()
+
+
+def spreader_program(type_id: int) -> np.ndarray:
+    """examples/spreader/main.pony:1-48 (the compiled GPU_ACTOR_HT_SPREADER,
+    engine_dev.h) for a program type `type_id`: word 0 count, 1 parent (~0:
+    the root), 2 _result, 3 _received, 4 the root's printed total.
+    Behaviour 0 SPREAD(parent << 32 | count) — the constructor — spawns two
+    children of its own type when count > 1 (SPAWN); behaviour 1 RESULT(i)."""
+    p = Program()
+    p.behaviour(0)                      # new create / new spread
+    p.ldi(11, 32)
+    p.ldi(12, -1)                       # GPU_ACTOR_NONE
+    p.shr(13, 12, 11)                   # 0xFFFFFFFF
+    p.and_(0, R_ARG, 13)                # count
+    p.shr(14, R_ARG, 11)                # parent
+    p.mov(1, 14)
+    p.eq(15, 14, 13)
+    p.jz(15, "has_parent")
+    p.mov(1, 12)                        # the root: parent = NONE
+    p.label("has_parent")
+    p.ldi(15, 2)
+    p.ltu(15, 0, 15)                    # count <= 1
+    p.jz(15, "spawn")
+    p.eq(15, 1, 12)
+    p.jnz(15, "root_leaf")
+    p.ldi(14, 1)
+    p.send(1, 1, 14)                    # RESULT(1) to the parent
+    p.halt()
+    p.label("root_leaf")
+    p.ldi(4, 1)                         # "1 actor"
+    p.halt()
+    p.label("spawn")
+    p.shl(14, R_SELF, 11)
+    p.addi(15, 0, -1)
+    p.or_(14, 14, 15)                   # self << 32 | count - 1
+    p.spawn(type_id, 0, 14)
+    p.spawn(type_id, 0, 14)
+    p.halt()
+    p.behaviour(1)                      # be result(i)
+    p.addi(3, 3, 1)
+    p.add(2, 2, R_ARG)
+    p.ldi(15, 2)
+    p.eq(15, 3, 15)
+    p.jz(15, "wait")
+    p.addi(14, 2, 1)
+    p.ldi(12, -1)
+    p.eq(15, 1, 12)
+    p.jnz(15, "root_total")
+    p.send(1, 1, 14)                    # RESULT(result + 1) to the parent
+    p.halt()
+    p.label("root_total")
+    p.mov(4, 14)                        # "<n> actors"
+    p.label("wait")
     p.halt()
     return p.assemble()

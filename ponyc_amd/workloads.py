@@ -232,6 +232,19 @@ def spreader(eng, count: int = 10, type_id: int = 0) -> dict:
     return {"type": type_id, "root": root, "nodes": nodes}
 
 
+def spreader_prog(eng, count: int = 10, type_id: int = 0) -> dict:
+    """`spreader` with the Spreader's behaviours as a program
+    (ponyc_amd.program.spreader_program): the children are created by the
+    program's SPAWN op."""
+    eng.type_register(type_id, 8, HT_PROGRAM)
+    eng.type_program(type_id, P.spreader_program(type_id))
+    nodes = (1 << count) - 1
+    eng.type_reserve(type_id, nodes - 1)
+    root = eng.create(type_id, 1)
+    _send(eng, root, SPREADER_SPREAD, (0xFFFFFFFF << 32) | count)
+    return {"type": type_id, "root": root, "nodes": nodes}
+
+
 def spreader_result(eng, w: dict) -> np.ndarray:
     """[count, parent, _result, _received, printed] of every actor, by id."""
     return eng.state_read(w["type"])

@@ -72,6 +72,21 @@ def test_det_program_equals_compiled(n, initial, hops, batch):
         assert cp[k] == cc[k], k
 
 
+@pytest.mark.parametrize("count", [1, 2, 6, 10])
+def test_spreader_program_equals_compiled(count):
+    """The SPAWN op (pony_create + the constructor message inside a
+    behaviour): the spreader as a program builds the same tree — every node's
+    state, the ids it gets, the counts and the step count — as the compiled
+    GPU_ACTOR_HT_SPREADER table."""
+    sc, cc, rc = _run(lambda e: W.spreader(e, count), W.spreader_result)
+    sp, cp, rp = _run(lambda e: W.spreader_prog(e, count),
+                      lambda e, w: e.state_read(w["type"])[0:5])
+    assert sp == sc
+    np.testing.assert_array_equal(rp, rc)
+    for k in ("delivered", "sent", "pending", "dropped"):
+        assert cp[k] == cc[k], k
+
+
 def edge_program() -> np.ndarray:
     """Behaviour 0: r0 += 1, a send past the world's ids (dropped), yield.
     Behaviour 1: a loop that never ends (stops after MAX_STEPS instructions,
