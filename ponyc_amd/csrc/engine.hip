@@ -28,6 +28,7 @@
 #include "sparse_dev.h"
 #include "hot_dev.h"
 #include "step_entry.h"
+#include "jit_host.h"
 
 // the 4096-actor-zone instantiations (step_*_z12.hip)
 namespace gpa_z12 {
@@ -276,7 +277,8 @@ struct HostType {
   uint64_t* d_state = nullptr;
   uint64_t* d_prog = nullptr;           // GPU_ACTOR_HT_PROGRAM: the behaviours' program
   uint32_t prog_n = 0;
-  bool prog_yields = false;             // it holds a YIELD: the small-step path leaves it
+  bool prog_yields = false;             // it holds a YIELD or a SPAWN: the small-step path leaves it
+  std::vector<uint64_t> prog_host;      // the program's words (the run-time compiled step, jit_host.h)
 };
 
 struct Engine {
@@ -328,6 +330,18 @@ struct Engine {
   uint64_t host_seq = 0;
   uint64_t steps_total = 0;
   int sticky = 0;
+  // behaviours as programs compiled at run time (jit_host.h): the module of
+  // the current program set and geometry, the set a build failed for (kept
+  // on the interpreter), the constants last uploaded (for a module loaded
+  // later), and how many modules were built or loaded
+  jit::Module jit;
+  uint64_t jit_set = 0;                 // the program set (and geometry) the module is for
+  uint64_t jit_failed = 0;
+  uint32_t jit_builds = 0;
+  bool jit_used = false;                // the last step ran the compiled module
+  TypeDev td_host[GPU_ACTOR_MAX_TYPES];
+  EngDev eng_host;
+  bool consts_host = false;
   // One rank: device work that can change the spill status or the counters
   // bumps dev_epoch; a host read of either records the epoch it saw, so a
   // read that nothing could have changed since is skipped (run_fixed's and
@@ -624,6 +638,14 @@ int upload_types()
   // every k_step code object holds its own copy of the constants
   for(const StepEntry& se : step_entries())
     HIPCK(se.upload(td, &e, g.stream));
+  memcpy(g.td_host, td, sizeof(td));
+  g.eng_host = e;
+  g.consts_host = true;
+  if(g.jit.mod)
+  {
+    HIPCK(hipMemcpyHtoDAsync(g.jit.types, g.td_host, sizeof(g.td_host), g.stream));
+    HIPCK(hipMemcpyHtoDAsync(g.jit.eng, &g.eng_host, sizeof(g.eng_host), g.stream));
+  }
   return 0;
 }
 
@@ -1389,6 +1411,7 @@ StepEntry step_entry_for(bool z12)
 }
 
 StepEntry pick_step_entry() { return step_entry_for(g.zbits == 12); }
+StepEntry step_entry_for_any(bool z12) { return z12 ? gpa_z12::step_entry_any() : gpa::step_entry_any(); }
 
 // LDS a workgroup may hold on gfx950 (the CU's whole 160 KB; two 512-thread
 // zones per CU at <= 80 KB each)
@@ -1531,6 +1554,77 @@ int spawn_process(uint32_t cur)
 }
 
 // One superstep: k_step on parity g.par (+ exchange), then flip parity.
+// The run-time compiled step this engine's tables take (jit_host.h), built
+// or loaded once per set (a set whose build fails stays on the compiled-in
+// kernels; one seen before in this process, or on disk, loads at once), with
+// PONYC_AMD_JIT not 0: 1 — every serial actor runs a program: the programs
+// compiled (two launches, PM 1 plain zones and PM 2 the rest, with the split
+// launches on); 2 — a mix of tables the any-mix kernel would run: that
+// kernel with only those tables' drains; 0 — neither.
+int step_after_launch(uint32_t slot, hipEvent_t e0, hipEvent_t e1);
+int jit_ensure(const StepEntry& se)
+{
+  const char* f = getenv("PONYC_AMD_JIT");
+  if((f && atoi(f) == 0) || !g.consts_host) return 0;
+  const bool z12 = g.zbits == 12;
+  std::vector<jit::Prog> progs;
+  uint32_t mask = 0;
+  bool all_prog = true;
+  for(uint32_t t = 0; t < GPU_ACTOR_MAX_TYPES; ++t)
+  {
+    const HostType& h = g.types[t];
+    if(!h.created || reducible_ht(h.ht)) continue;
+    mask |= 1u << h.ht;
+    if(h.ht != GPU_ACTOR_HT_PROGRAM || h.prog_host.empty()) all_prog = false;
+    else progs.push_back({t, h.prog_host});
+  }
+  int kind = 0;
+  uint64_t want = jit::fnv1a(z12 ? "z12" : "z11");
+  if(all_prog && !progs.empty() && g.split_plan)
+  {
+    kind = 1;
+    for(const jit::Prog& p : progs)
+      want = jit::fnv1a(std::string(reinterpret_cast<const char*>(p.code.data()), p.code.size() * 8),
+                        jit::fnv1a(std::to_string(p.type), want));
+  }
+  else if(se.kernel == step_entry_for_any(z12).kernel && mask)
+  {
+    kind = 2;
+    want = jit::fnv1a("mix" + std::to_string(mask), want);
+  }
+  if(!kind) return 0;
+  if(g.jit.mod && g.jit_set == want) return kind;
+  if(g.jit_failed == want) return 0;
+  jit::unload(g.jit);
+  hipDeviceProp_t prop;
+  if(hipGetDeviceProperties(&prop, g.device) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  std::string arch = prop.gcnArchName;
+  arch = arch.substr(0, arch.find(':'));
+  std::string log;
+  const int rc = kind == 1 ? jit::build(progs, z12, arch, g.jit, log)
+                           : jit::build_mix(mask, z12, arch, g.jit, log);
+  if(getenv("PONYC_AMD_JIT_LOG"))
+    fprintf(stderr, "gpu_actor jit: %s %s%s (rc %d) %s\n", kind == 1 ? "programs" : "mix",
+            kind == 2 ? ("mask " + std::to_string(mask) + " ").c_str() : "", z12 ? "z12" : "z11", rc,
+            log.c_str());
+  if(rc != 0)
+  {
+    g.jit_failed = want;
+    return 0;
+  }
+  g.jit_set = want;
+  g.jit_builds++;
+  if(hipMemcpyHtoDAsync(g.jit.types, g.td_host, sizeof(g.td_host), g.stream) != hipSuccess ||
+     hipMemcpyHtoDAsync(g.jit.eng, &g.eng_host, sizeof(g.eng_host), g.stream) != hipSuccess)
+  {
+    (void)hipGetLastError();
+    jit::unload(g.jit);
+    g.jit_failed = want;
+    return 0;
+  }
+  return kind;
+}
+
 int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
 {
   if(g.n_zones == 0) return 0;
@@ -1542,6 +1636,30 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   const uint64_t nb = g.n_zones + (R() > 1 ? R() : 0);
   if(!step_fits(se, nb)) return GPU_ACTOR_ERANGE;    // more buckets than a workgroup's LDS holds
   const size_t dyn = step_dyn_bytes(se, nb);
+  // the run-time compiled step (jit_ensure), when it builds and fits: the
+  // programs' as two launches like the interpreter's, or a mix's one launch
+  // with k_hot before it where hot zones are prepared
+  g.jit_used = false;
+  const int jk = jit_ensure(se);
+  if(jk && g.jit.static_lds + dyn <= kLdsPerWorkgroup)
+  {
+    g.jit_used = true;
+    uint32_t a_cur = g.par, a_slot = slot, a_sidx = g.sidx;
+    void* args[] = {&a_cur, &a_slot, &a_sidx};
+    if(e0) HIPCK(hipEventRecord(e0, g.stream));
+    if(jk == 2 && g.hot_on)
+      hipLaunchKernelGGL(k_hot, dim3(kHotBlocks), dim3(kHotThreads), 5u * zone_actors() * sizeof(uint32_t),
+        g.stream, g.par, g.sidx);
+    HIPCK(hipModuleLaunchKernel(g.jit.plan, g.n_zones, 1, 1, se.threads, 1, 1, (unsigned)dyn, g.stream,
+      args, nullptr));
+    if(jk == 1)
+      HIPCK(hipModuleLaunchKernel(g.jit.rest, g.n_zones, 1, 1, se.threads, 1, 1, (unsigned)dyn, g.stream,
+        args, nullptr));
+    if(g.defer_big)
+      hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream, g.par);
+    if(e1) HIPCK(hipEventRecord(e1, g.stream));
+    return step_after_launch(slot, e0, e1);
+  }
   // a two-pass table's step as two launches: its two-pass zones, then the rest
   // (zone_dev.h k_step PM)
   // (fused: one launch of PM 3 in their place)
@@ -1577,6 +1695,14 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
     if(g.defer_big)
       hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream, g.par);
   }
+  HIPCK(hipGetLastError());
+  return step_after_launch(slot, e0, e1);
+}
+
+// After a step's launches: the parity and step index advance; the exchange
+// (n_ranks > 1), the halted step's rerun, spawned actors.
+int step_after_launch(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
+{
   HIPCK(hipGetLastError());
   const uint32_t step_sidx = g.sidx;
   g.par ^= 1u;
@@ -1647,6 +1773,10 @@ int ensure_events(size_t n)
 
 void free_all()
 {
+  jit::unload(g.jit);
+  g.jit_set = g.jit_failed = 0;
+  g.jit_builds = 0;
+  g.jit_used = g.consts_host = false;
   for(auto& t : g.types)
   {
     if(t.d_state) (void)hipFree(t.d_state);
@@ -2098,9 +2228,10 @@ GPU_ACTOR_API int gpu_actor_type_program(uint32_t type_id, const uint64_t* code,
   }
   t.d_prog = d;
   t.prog_n = n;
+  t.prog_host.assign(code, code + n);
   t.prog_yields = false;
-  for(uint32_t k = GPU_ACTOR_PROG_ENTRIES; k < n; ++k)
-    t.prog_yields |= (code[k] & 0xFFu) == GPU_ACTOR_OP_YIELD;
+  for(uint32_t k = 0; k < n; ++k)                   // (a jump may run the entry words too)
+    t.prog_yields |= (code[k] & 0xFFu) == GPU_ACTOR_OP_YIELD || (code[k] & 0xFFu) == GPU_ACTOR_OP_SPAWN;
   return t.created ? upload_types() : 0;
 }
 
@@ -2697,9 +2828,57 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
     HIPCK(hipMemcpyAsync(hb, hot_bar_words(), sizeof(hb), hipMemcpyDeviceToHost, g.stream));
     HIPCK(hipStreamSynchronize(g.stream));
   }
-  const uint64_t v[12] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
-                          g.n_zones, tn[0], tn[1], tn[2], g.zbits, hb[3], g.hot_on ? 1u : 0u};
-  for(uint64_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
+  // + [12] whether the last step ran the module compiled from the programs
+  // (jit_host.h), [13] modules built or loaded by this engine
+  const uint64_t v[14] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+                          g.n_zones, tn[0], tn[1], tn[2], g.zbits, hb[3], g.hot_on ? 1u : 0u,
+                          g.jit_used ? 1u : 0u, g.jit_builds};
+  for(uint64_t i = 0; i < n && i < 14; ++i) out[i] = v[i];
+  return 0;
+}
+
+// Diagnostic (not in the public header): compile the step for a program set
+// into the code-object cache (jit_host.h) without a device — `nprog` programs,
+// types[k] running words[off_k, off_k + lens[k]) (concatenated), at the
+// 4096-actor geometry when z12 — so that a later run loads it at once.
+// Returns 0, or GPU_ACTOR_EINVAL with hiprtc's log on stderr.
+GPU_ACTOR_API int gpu_actor_debug_jit_compile(const uint32_t* types, const uint64_t* words,
+  const uint32_t* lens, uint32_t nprog, int z12, const char* arch)
+{
+  if(!types || !words || !lens || nprog == 0 || nprog > GPU_ACTOR_MAX_TYPES) return GPU_ACTOR_EINVAL;
+  std::vector<jit::Prog> progs;
+  uint64_t off = 0;
+  for(uint32_t k = 0; k < nprog; ++k)
+  {
+    if(lens[k] <= GPU_ACTOR_PROG_ENTRIES || lens[k] > jit::kMaxWords) return GPU_ACTOR_EINVAL;
+    progs.push_back({types[k], std::vector<uint64_t>(words + off, words + off + lens[k])});
+    off += lens[k];
+  }
+  const std::string src = jit::unit_source(progs, z12 != 0);
+  const std::string a = arch && *arch ? arch : "gfx950";
+  std::string log;
+  const std::string co = jit::code_object(src, a, jit::key_of(src, a), log);
+  if(co.empty())
+  {
+    fprintf(stderr, "gpu_actor jit: %s\n", log.c_str());
+    return GPU_ACTOR_EINVAL;
+  }
+  return 0;
+}
+
+// Diagnostic (not in the public header): the same for the any-mix step of a
+// mix of compiled tables (bit per table id, jit_host.h build_mix).
+GPU_ACTOR_API int gpu_actor_debug_jit_compile_mix(uint32_t mask, int z12, const char* arch)
+{
+  if(mask == 0) return GPU_ACTOR_EINVAL;
+  const std::string src = jit::mix_source(mask, z12 != 0);
+  const std::string a = arch && *arch ? arch : "gfx950";
+  std::string log;
+  if(jit::code_object(src, a, jit::key_of(src, a), log).empty())
+  {
+    fprintf(stderr, "gpu_actor jit: %s\n", log.c_str());
+    return GPU_ACTOR_EINVAL;
+  }
   return 0;
 }
 

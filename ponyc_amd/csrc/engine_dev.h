@@ -17,8 +17,8 @@
 #pragma once
 #ifndef __HIPCC_RTC__       // (also compiled at run time: engine.hip jit)
 #include <hip/hip_runtime.h>
-#include <stdint.h>
 #endif
+#include <stdint.h>
 #include "../../include/gpu_actor.h"
 #include "rng_dev.h"
 

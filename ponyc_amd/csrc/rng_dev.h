@@ -4,8 +4,8 @@
 #pragma once
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
-#include <stdint.h>
 #endif
+#include <stdint.h>
 
 namespace gpa {
 

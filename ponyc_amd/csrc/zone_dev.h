@@ -63,10 +63,13 @@ static_assert(kHotMin > kIdxCap, "hot zones take the scratch path");
 // 16 where the handler does not read the message (pinger: the selection
 // compiles away) or the table's state is small; 8 elsewhere, to stay within
 // 128 VGPRs without spilling.
+// (the run-time compiled program table, kHtJit: its generated code keeps the
+// program's registers as locals, so it holds as many as the compiled tables)
 template <int HT> __host__ __device__ constexpr uint32_t small_regs()
 {
   return (HT == GPU_ACTOR_HT_PINGER || HT == GPU_ACTOR_HT_FANIN_SENDER ||
-          HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM) ? 16u : HT == GPU_ACTOR_HT_PROGRAM ? 4u : 8u;
+          HT == GPU_ACTOR_HT_PINGER_DET || HT == GPU_ACTOR_HT_STORM || HT == kHtJit) ? 16u
+         : HT == GPU_ACTOR_HT_PROGRAM ? 4u : 8u;
 }
 
 // A workgroup barrier that orders LDS only. __syncthreads() also waits for
@@ -365,6 +368,12 @@ constexpr uint32_t kMedReg = 16;
 // A table whose behaviours ignore the message (the message-ubench pinger:
 // every ping has the same effect) needs no delivery order; the compiler then
 // drops the key selection of its drain entirely.
+// The tables the any-mix kernel compiles (all; a run-time compiled mix,
+// jit_host.h, only the engine's)
+#ifndef GPA_MIX_MASK
+#define GPA_MIX_MASK 0xFFFFFFFFu
+#endif
+
 template <int HT> __host__ __device__ constexpr bool order_free()
 {
   return HT == GPU_ACTOR_HT_PINGER;
@@ -408,9 +417,13 @@ template <int HT> __host__ __device__ constexpr uint32_t seq_batch()
   return (HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_FIFO_SRC) ? 4u : 1u;
 }
 
+// (kHtJit: when the compiled program set holds a YIELD, jit_host.h)
+#ifndef GPA_JIT_YIELD
+#define GPA_JIT_YIELD 1
+#endif
 template <int HT> __host__ __device__ constexpr bool may_yield()
 {
-  return HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_PROGRAM || HT == kHtJit;
+  return HT == GPU_ACTOR_HT_FIFO_SINK || HT == GPU_ACTOR_HT_PROGRAM || (HT == kHtJit && GPA_JIT_YIELD);
 }
 
 // Drain one actor: handle up to min(batch, n) messages — carried mail, then
@@ -1397,7 +1410,8 @@ template <int HTS> struct ZoneLds {
     struct { uint32_t stl[kMaxStage], stc[kMaxStage], sto[kMaxStage + 1]; } st;   // staged runs
     unsigned long long red[kZoneWaves][6];
   } u;
-  unsigned long long fan[(HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER) ? 2 * kFanLds : 1];   // fan-in apply accumulators
+  unsigned long long fan[((HTS < 0 && ((GPA_MIX_MASK >> GPU_ACTOR_HT_FANIN_SENDER) & 1u)) ||
+                          HTS == GPU_ACTOR_HT_FANIN_SENDER) ? 2 * kFanLds : 1];   // fan-in apply accumulators
 };
 template <int HTS> __device__ __forceinline__ ZoneLds<HTS>& zone_lds()
 {
@@ -1441,7 +1455,8 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
   auto& s_stc = Z.u.st.stc;
   auto& s_sto = Z.u.st.sto;
   auto& s_fan = Z.fan;
-  constexpr bool kFan = HTS < 0 || HTS == GPU_ACTOR_HT_FANIN_SENDER;
+  constexpr bool kFan = (HTS < 0 && ((GPA_MIX_MASK >> GPU_ACTOR_HT_FANIN_SENDER) & 1u)) ||
+                        HTS == GPU_ACTOR_HT_FANIN_SENDER;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   static_assert(PM == 0 || HTS >= 0, "split launches are for one-table engines");
@@ -2432,7 +2447,9 @@ __device__ __forceinline__ bool zone_step(const uint32_t z, uint32_t cur, uint32
     {
       switch(T.ht)
       {
-#define ZCASE(HT) case HT: { ZDRAIN(HT) } break;
+// (GPA_MIX_MASK: the tables a run-time compiled any-mix step holds, bit
+// per table id — engine.hip jit; the others' cases are not compiled)
+#define ZCASE(HT) case HT: if constexpr(((GPA_MIX_MASK) >> (HT)) & 1u) { ZDRAIN(HT) } break;
         ZCASE(GPU_ACTOR_HT_RING)
         ZCASE(GPU_ACTOR_HT_PINGER)
         ZCASE(GPU_ACTOR_HT_PINGER_DET)

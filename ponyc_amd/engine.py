@@ -44,7 +44,11 @@ ERRORS = {
 class GpuActorError(RuntimeError):
     def __init__(self, fn: str, code: int):
         super().__init__(f"{fn} failed: {ERRORS.get(code, code)} ({code})")
+        self.fn = fn
         self.code = code
+
+    def __reduce__(self):              # (crosses process pools)
+        return (GpuActorError, (self.fn, self.code))
 
 
 class Config(ctypes.Structure):
@@ -372,7 +376,8 @@ class Engine:
     def debug_info(self) -> dict:
         """Engine internals (diagnostic export, not in include/gpu_actor.h)."""
         keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones",
-                "trig_n0", "trig_n1", "trig_n2", "zone_bits", "hot_missed", "hot_on"]
+                "trig_n0", "trig_n1", "trig_n2", "zone_bits", "hot_missed", "hot_on", "jit",
+                "jit_builds"]
         out = (ctypes.c_uint64 * len(keys))()
         fn = self.lib.gpu_actor_debug_info
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
@@ -398,3 +403,30 @@ class Engine:
 
     def __exit__(self, *exc):
         self.shutdown()
+
+
+def jit_compile(progs, z12: bool = False, arch: str = "gfx950", lib_path: str | None = None) -> None:
+    """Compile the step for a program set (`progs`: [(type id, words), ...])
+    into the library's code-object cache without a device (csrc/jit_host.h;
+    diagnostic export gpu_actor_debug_jit_compile), so that an engine running
+    these programs loads it at once."""
+    lib = ctypes.CDLL(lib_path or LIB_PATH)
+    fn = lib.gpu_actor_debug_jit_compile
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                   ctypes.c_char_p]
+    fn.restype = ctypes.c_int
+    types = np.array([t for t, _ in progs], dtype=np.uint32)
+    words = np.concatenate([np.asarray(w, dtype=np.uint64) for _, w in progs])
+    lens = np.array([len(w) for _, w in progs], dtype=np.uint32)
+    _ck("gpu_actor_debug_jit_compile", fn(types.ctypes.data, words.ctypes.data, lens.ctypes.data,
+                                          len(progs), int(z12), arch.encode()))
+
+
+def jit_compile_mix(mask: int, z12: bool = False, arch: str = "gfx950", lib_path: str | None = None) -> None:
+    """The same for the any-mix step of a mix of compiled tables (`mask`: bit
+    per table id; gpu_actor_debug_jit_compile_mix)."""
+    lib = ctypes.CDLL(lib_path or LIB_PATH)
+    fn = lib.gpu_actor_debug_jit_compile_mix
+    fn.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p]
+    fn.restype = ctypes.c_int
+    _ck("gpu_actor_debug_jit_compile_mix", fn(mask, int(z12), arch.encode()))

@@ -207,9 +207,19 @@ def test_spreader_matches_reference_golden(engine_factory):
     assert e.type_live(w["type"]) == w["nodes"]
 
 
-def test_spreader_after_other_types(engine_factory, oracle):
+@pytest.mark.parametrize("jit", ["1", "0"])
+def test_spreader_after_other_types(engine_factory, oracle, monkeypatch, jit):
     """Spawned ids sit inside their own type's range with other types around
-    it; the ring's traffic runs in the same steps."""
+    it; the ring's traffic runs in the same steps. A mix of tables: the
+    any-mix step compiled at run time for this mix (csrc/jit_host.h,
+    PONYC_AMD_JIT=1) or the compiled-in any-mix kernel (0)."""
+    monkeypatch.setenv("PONYC_AMD_JIT", jit)
+    made = []
+
+    def factory(**kw):
+        e = engine_factory(**kw)
+        made.append(e)
+        return e
     def setup(e):
         r = W.ring(e, 100, 3, 50, type_id=0)
         s = W.spreader(e, 9, type_id=1)
@@ -219,8 +229,9 @@ def test_spreader_after_other_types(engine_factory, oracle):
         r, s = w
         return np.concatenate([W.ring_result(e, r).ravel(), W.spreader_result(e, s).ravel(),
                                e.state_read(2).ravel()])
-    g, o = _both(engine_factory, oracle, setup, result)
+    g, o = _both(factory, oracle, setup, result)
     _assert_same(g, o)
+    assert (made[0].debug_info()["jit_builds"] >= 1) == (jit == "1")
 
 
 def test_spreader_reserve_exhausted(engine_factory):
