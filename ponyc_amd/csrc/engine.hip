@@ -342,6 +342,14 @@ struct Engine {
   TypeDev td_host[GPU_ACTOR_MAX_TYPES];
   EngDev eng_host;
   bool consts_host = false;
+  // GUPS streamers' chunks for k_gups_apply (EngDev::gups_*; gups_type -1: none)
+  uint64_t* d_gups_list = nullptr;
+  unsigned int* d_gups_n = nullptr;
+  uint64_t* d_gups_jump = nullptr;
+  unsigned long long* d_gups_stat = nullptr;
+  uint64_t gups_jump_host[65] = {};
+  uint32_t gups_cap = 0;
+  int gups_type = -1;
   // One rank: device work that can change the spill status or the counters
   // bumps dev_epoch; a host read of either records the epoch it saw, so a
   // read that nothing could have changed since is skipped (run_fixed's and
@@ -542,6 +550,80 @@ bool hot_resident()
   return cached != 0;
 }
 
+constexpr uint32_t kGupsBlocks = 1024;
+__global__ void __launch_bounds__(256) k_gups_apply();
+
+// The GUPS streamer type whose chunks k_gups_apply makes (EngDev::gups_*): the
+// first with a nonzero chunk, on one rank (PONYC_AMD_GUPS_DEFER=0: none, every
+// streamer applies its own chunk, for A/B runs). Chunks of L >= 16 updates per
+// lane, at most 64 lanes per chunk.
+int gups_setup(EngDev& e)
+{
+  g.gups_type = -1;
+  e.gups_type = -1;
+  const char* f = getenv("PONYC_AMD_GUPS_DEFER");
+  if(R() != 1 || (f && atoi(f) == 0)) return 0;
+  int t_def = -1;
+  for(uint32_t t = 0; t < GPU_ACTOR_MAX_TYPES && t_def < 0; ++t)
+    if(g.types[t].created && g.types[t].ht == GPU_ACTOR_HT_GUPS_STREAMER && g.types[t].params[0] > 0 &&
+       g.types[t].params[0] <= 0xFFFFFFFFull)
+      t_def = (int)t;
+  if(t_def < 0) return 0;
+  const HostType& h = g.types[t_def];
+  const uint64_t chunk = h.params[0];
+  const uint64_t L = std::max<uint64_t>(16, (chunk + 63) / 64);
+  const uint64_t parts = (chunk + L - 1) / L;
+  // kGupsShards segments, each at least 2^16 chunks (k_sparse lists from its
+  // few waves' segments only)
+  const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 22, 2ull * h.lcount), 1ull << 28);
+  if(cap > g.gups_cap)
+  {
+    HIPCK(hipStreamSynchronize(g.stream));      // no k_gups_apply still reads the old list
+    if(g.d_gups_list) HIPCK(hipFree(g.d_gups_list));
+    g.d_gups_list = nullptr;
+    g.gups_cap = 0;
+    HIPCK(hipMalloc(&g.d_gups_list, cap * sizeof(uint64_t)));
+    g.gups_cap = (uint32_t)cap;
+  }
+  if(!g.d_gups_n)
+  {
+    HIPCK(hipMalloc(&g.d_gups_n, (kGupsShards + 1) * sizeof(unsigned int)));
+    HIPCK(hipMemsetAsync(g.d_gups_n, 0, (kGupsShards + 1) * sizeof(unsigned int), g.stream));
+    HIPCK(hipMalloc(&g.d_gups_jump, 65 * sizeof(uint64_t)));
+    HIPCK(hipMalloc(&g.d_gups_stat, 2 * kGupsBlocks * sizeof(unsigned long long)));
+    HIPCK(hipMemsetAsync(g.d_gups_stat, 0, 2 * kGupsBlocks * sizeof(unsigned long long), g.stream));
+  }
+  uint64_t jump[65] = {};
+  for(uint64_t p = 0; p < parts; ++p) jump[p] = gpa::polyrand_xpow(p * L);
+  jump[parts] = gpa::polyrand_xpow(chunk);
+  if(memcmp(jump, g.gups_jump_host, sizeof(jump)) != 0)
+  {
+    HIPCK(hipStreamSynchronize(g.stream));      // no launch still reads the old table
+    memcpy(g.gups_jump_host, jump, sizeof(jump));
+    HIPCK(hipMemcpyAsync(g.d_gups_jump, g.gups_jump_host, sizeof(jump), hipMemcpyHostToDevice,
+      g.stream));
+  }
+  e.gups_list = g.d_gups_list; e.gups_n = g.d_gups_n; e.gups_jump = g.d_gups_jump;
+  e.gups_stat = g.d_gups_stat;
+  e.gups_seg = g.gups_cap / kGupsShards; e.gups_l = (uint32_t)L; e.gups_parts = (uint32_t)parts;
+  e.gups_type = t_def;
+  g.gups_type = t_def;
+  return 0;
+}
+
+// k_gups_apply behind a step's kernels (engines with a chunk-listing streamer
+// type); the events, when given, end at its end
+int gups_apply_launch(hipEvent_t e1)
+{
+  if(g.gups_type < 0) return 0;
+  if(e1)
+    hipExtLaunchKernelGGL(k_gups_apply, dim3(kGupsBlocks), dim3(256), 0, g.stream, nullptr, e1, 0u);
+  else
+    hipLaunchKernelGGL(k_gups_apply, dim3(kGupsBlocks), dim3(256), 0, g.stream);
+  HIPCK(hipGetLastError());
+  return 0;
+}
+
 int upload_types()
 {
   TypeDev td[GPU_ACTOR_MAX_TYPES];
@@ -633,6 +715,10 @@ int upload_types()
     g.fuse = !(fu && atoi(fu) == 0);
   }
   e.zplan = g.d_zplan;
+  {
+    const int rc = gups_setup(e);
+    if(rc) return rc;
+  }
   HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_eng), &e, sizeof(e), 0,
     hipMemcpyHostToDevice, g.stream));
   // every k_step code object holds its own copy of the constants
@@ -1039,6 +1125,130 @@ __global__ void k_spill_flag(unsigned int* flag)
 // This rank's spill status as one number (zone spill lists, halt, and the
 // summed flag of the last exchange): summed over ranks by pend_read, it is
 // the same on every rank, so every rank decides alike whether to fix up.
+// The GUPS streamers' chunks listed since the last launch (EngDev::gups_list,
+// one rank): gups_parts lanes per chunk, 64 / gups_parts chunks per wave; lane
+// p regenerates updates p * L + 1 .. (p + 1) * L of its chunk (L = gups_l)
+// from state * x^(p * L) — one GF(2) product, PolyRand._seed's own jump
+// (gups_basic/main.pony:182-216) — and XORs each into its updater's word
+// (Updater.apply, main.pony:145-155). Per update instruction the wave combines
+// the lanes that share the first (then the second) remaining lane's word into
+// one atomic, and issues no atomic for an XOR of 0 (the identity: a stream
+// _seed left at 0 repeats word 0 of updater 0). The last workgroup to finish
+// empties the list.
+__global__ void __launch_bounds__(256) k_gups_apply()
+{
+  // the segments' chunk counts, and their prefix: chunk e (in segment order)
+  // is entry e - s_pre[s] of the segment s with s_pre[s] <= e < s_pre[s + 1]
+  __shared__ uint32_t s_pre[kGupsShards + 1];
+  if(threadIdx.x < kGupsShards)
+  {
+    uint32_t c = min(__atomic_load_n(&c_eng.gups_n[threadIdx.x], __ATOMIC_RELAXED), c_eng.gups_seg);
+    for(int off = 1; off < (int)kGupsShards; off <<= 1)
+    {
+      const uint32_t o = __shfl_up(c, off);
+      if((int)threadIdx.x >= off) c += o;
+    }
+    s_pre[threadIdx.x + 1] = c;
+    if(threadIdx.x == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t n = s_pre[kGupsShards];
+  const TypeDev& S = c_types[c_eng.gups_type];
+  const uint64_t chunk = S.params[0], shift = S.params[1], mask = S.params[2];
+  const uint32_t ubase = (uint32_t)S.params[3];
+  const uint32_t L = c_eng.gups_l, parts = c_eng.gups_parts, per_wave = 64u / parts;
+  const uint32_t lane = threadIdx.x & 63u, sub = lane / parts, p = lane - sub * parts;
+  const uint64_t jump = c_eng.gups_jump[p];
+  const uint64_t first = (uint64_t)p * L;
+  const uint32_t cnt = first < chunk ? (uint32_t)min<uint64_t>(L, chunk - first) : 0u;
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  // the updater type last written (gups updaters are one type in practice)
+  uint32_t u_first = 0, u_count = 0, u_lfirst = 0, u_lcount = 0;
+  uint64_t* u_state = nullptr;
+  uint64_t u_mask = 0;
+  uint32_t made = 0, issued = 0;
+  for(uint64_t e0 = wave * per_wave; e0 < n; e0 += waves * per_wave)
+  {
+    const uint64_t e = e0 + sub;
+    const bool live = sub < per_wave && e < n;
+    uint64_t v = 0;
+    if(live)
+    {
+      uint32_t lo = 0, hi = kGupsShards;
+      while(hi - lo > 1u)
+      {
+        const uint32_t mid = (lo + hi) >> 1;
+        if(s_pre[mid] <= e) lo = mid; else hi = mid;
+      }
+      v = c_eng.gups_list[(size_t)lo * c_eng.gups_seg + (e - s_pre[lo])];
+    }
+    if(live && p) v = polyrand_mulmod(v, jump);
+    for(uint32_t j = 0; j < L; ++j)
+    {
+      unsigned long long* w = nullptr;
+      if(live && j < cnt)
+      {
+        (void)polyrand_next(v);
+        ++made;
+        const uint32_t to = ubase + (uint32_t)((v >> shift) & mask);
+        if(to - u_first >= u_count)
+        {
+          const int t = type_of_global(to);
+          if(t >= 0)
+          {
+            const TypeDev& U = c_types[t];
+            u_first = U.first; u_count = U.count; u_lfirst = U.lfirst; u_lcount = U.lcount;
+            u_state = U.state; u_mask = U.params[0] - 1;
+          }
+        }
+        if(to - u_first < u_count)
+          w = reinterpret_cast<unsigned long long*>(&u_state[(v & u_mask) * u_lcount + (to - u_lfirst)]);
+      }
+      // the wave's update instruction: up to two combined words, then the rest
+      const uint64_t wa = reinterpret_cast<uint64_t>(w);
+      uint64_t left = __ballot(w != nullptr);
+      for(int round = 0; round < 2 && left; ++round)
+      {
+        const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1u;
+        const uint64_t lw = __shfl(wa, (int)lead);
+        const uint64_t peers = __ballot(((left >> lane) & 1ull) && wa == lw);
+        uint64_t r = ((peers >> lane) & 1ull) ? v : 0ull;
+        if(__popcll(peers) > 1)
+          for(int off = 32; off; off >>= 1) r ^= __shfl_xor(r, off);
+        if(lane == lead && r != 0)
+        {
+          atomicXor(w, (unsigned long long)r);
+          ++issued;
+        }
+        left &= ~peers;
+      }
+      if(((left >> lane) & 1ull) && v != 0)
+      {
+        atomicXor(w, (unsigned long long)v);
+        ++issued;
+      }
+    }
+  }
+  // per workgroup: updates made, atomics issued (each slot written by its own
+  // workgroup only, summed by the host)
+  __shared__ uint32_t s_sum[2];
+  if(threadIdx.x < 2) s_sum[threadIdx.x] = 0;
+  __syncthreads();
+  if(made) atomicAdd(&s_sum[0], made);
+  if(issued) atomicAdd(&s_sum[1], issued);
+  __syncthreads();
+  if(threadIdx.x == 0)
+  {
+    c_eng.gups_stat[blockIdx.x] += s_sum[0];
+    c_eng.gups_stat[kGupsBlocks + blockIdx.x] += s_sum[1];
+    __threadfence();
+    const unsigned int done = atomicAdd(&c_eng.gups_n[kGupsShards], 1u);
+    if(done == gridDim.x - 1u)
+      for(uint32_t s = 0; s <= kGupsShards; ++s) atomicExch(&c_eng.gups_n[s], 0u);
+  }
+}
+
 __global__ void k_spill_local(unsigned long long* out)
 {
   *out = (unsigned long long)c_eng.spill_n[0] + c_eng.spill_n[1] + *c_eng.halt +
@@ -1657,6 +1867,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
         args, nullptr));
     if(g.defer_big)
       hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream, g.par);
+    const int grc = gups_apply_launch(nullptr);
+    if(grc) return grc;
     if(e1) HIPCK(hipEventRecord(e1, g.stream));
     return step_after_launch(slot, e0, e1);
   }
@@ -1672,7 +1884,8 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
   {
     // the events take the dispatch's own start/end timestamps: no marker
     // packets between steps
-    const bool more = split || g.defer_big;
+    const bool gups = g.gups_type >= 0;
+    const bool more = split || g.defer_big || gups;
     if(g.hot_on)
       hipExtLaunchKernelGGL(k_hot, dim3(kHotBlocks), dim3(kHotThreads), (uint32_t)hot_lds, g.stream,
         e0, nullptr, 0u, g.par, g.sidx);
@@ -1680,10 +1893,13 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
       g.hot_on ? nullptr : e0, more ? nullptr : e1, 0u, g.par, slot, g.sidx);
     if(split)
       hipExtLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), (uint32_t)dyn, g.stream,
-        nullptr, g.defer_big ? nullptr : e1, 0u, g.par, slot, g.sidx);
+        nullptr, (g.defer_big || gups) ? nullptr : e1, 0u, g.par, slot, g.sidx);
     if(g.defer_big)
       hipExtLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream,
-        nullptr, e1, 0u, g.par);
+        nullptr, gups ? nullptr : e1, 0u, g.par);
+    HIPCK(hipGetLastError());
+    const int grc = gups_apply_launch(e1);
+    if(grc) return grc;
   }
   else
   {
@@ -1694,6 +1910,9 @@ int launch_step(uint32_t slot, hipEvent_t e0, hipEvent_t e1)
       hipLaunchKernelGGL(se.rest, dim3(g.n_zones), dim3(se.threads), dyn, g.stream, g.par, slot, g.sidx);
     if(g.defer_big)
       hipLaunchKernelGGL(k_carry_big, dim3(kBigCopyBlocks), dim3(kBlock), 0, g.stream, g.par);
+    HIPCK(hipGetLastError());
+    const int grc = gups_apply_launch(nullptr);
+    if(grc) return grc;
   }
   HIPCK(hipGetLastError());
   return step_after_launch(slot, e0, e1);
@@ -1777,6 +1996,14 @@ void free_all()
   g.jit_set = g.jit_failed = 0;
   g.jit_builds = 0;
   g.jit_used = g.consts_host = false;
+  if(g.d_gups_list) (void)hipFree(g.d_gups_list);
+  if(g.d_gups_n) (void)hipFree(g.d_gups_n);
+  if(g.d_gups_jump) (void)hipFree(g.d_gups_jump);
+  if(g.d_gups_stat) (void)hipFree(g.d_gups_stat);
+  g.d_gups_list = nullptr; g.d_gups_n = nullptr; g.d_gups_jump = nullptr; g.d_gups_stat = nullptr;
+  memset(g.gups_jump_host, 0, sizeof(g.gups_jump_host));
+  g.gups_cap = 0;
+  g.gups_type = -1;
   for(auto& t : g.types)
   {
     if(t.d_state) (void)hipFree(t.d_state);
@@ -2385,6 +2612,11 @@ int run_sparse(uint64_t max_steps, SparseCtl& out)
     hipLaunchKernelGGL(k_sparse<false>, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
       (unsigned long long)max_steps, g.d_ctl, g.sidx);
   HIPCK(hipGetLastError());
+  {
+    // the chunks its supersteps listed (2^16 or more per segment)
+    const int rc = gups_apply_launch(nullptr);
+    if(rc) return rc;
+  }
   HIPCK(hipMemcpyAsync(g.h_ctl, g.d_ctl, sizeof(SparseCtl), hipMemcpyDeviceToHost, g.stream));
   HIPCK(hipMemcpyAsync(g.h_sstat, g.d_sstat, sizeof(Engine::SpillStat), hipMemcpyDeviceToHost,
     g.stream));
@@ -2631,7 +2863,8 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   double ms_total = 0.0;
   while(left)
   {
-    rc = pend_clear(0, kPendSlots);
+    // only the slots these launches add to (slot kPendPre is written whole)
+    rc = pend_clear(0, (uint32_t)std::min<uint64_t>(left, kPendPre));
     if(rc) return rc;
     const uint32_t par0 = g.par, sidx0 = g.sidx;
     HIPCK(hipEventRecord(g.ev[0], g.stream));
@@ -2830,10 +3063,20 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
   }
   // + [12] whether the last step ran the module compiled from the programs
   // (jit_host.h), [13] modules built or loaded by this engine
-  const uint64_t v[14] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+  // + [14] updates k_gups_apply made, [15] the atomics it issued for them
+  uint64_t gu[2] = {0, 0};
+  if(g.d_gups_stat)
+  {
+    std::vector<unsigned long long> st(2 * kGupsBlocks);
+    HIPCK(hipMemcpyAsync(st.data(), g.d_gups_stat, st.size() * sizeof(unsigned long long),
+      hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    for(uint32_t b = 0; b < kGupsBlocks; ++b) { gu[0] += st[b]; gu[1] += st[kGupsBlocks + b]; }
+  }
+  const uint64_t v[16] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
                           g.n_zones, tn[0], tn[1], tn[2], g.zbits, hb[3], g.hot_on ? 1u : 0u,
-                          g.jit_used ? 1u : 0u, g.jit_builds};
-  for(uint64_t i = 0; i < n && i < 14; ++i) out[i] = v[i];
+                          g.jit_used ? 1u : 0u, g.jit_builds, gu[0], gu[1]};
+  for(uint64_t i = 0; i < n && i < 16; ++i) out[i] = v[i];
   return 0;
 }
 

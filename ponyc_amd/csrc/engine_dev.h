@@ -232,7 +232,28 @@ struct EngDev {
   uint32_t* hot_bcnt;
   uint32_t* hot_cur;
   uint32_t* hot_bar;
+  // GUPS streamers' chunks handed to the whole GPU (one rank, DESIGN.md §7
+  // C4): a streamer of type gups_type (-1: none) lists its PolyRand state
+  // before the chunk in gups_list and moves past the chunk with one jump
+  // (gups_jump[gups_parts] = x^chunk); k_gups_apply, launched behind every
+  // step, regenerates each chunk over gups_parts lanes, lane p from state *
+  // gups_jump[p] (= x^(p * gups_l)), and applies it. The list is kGupsShards
+  // segments of gups_seg chunks, a wave listing into segment (its global wave
+  // index mod kGupsShards): one counter for 16,384 listing waves per step
+  // serialised at the memory-side atomic unit (~13 ns each, 210 us of a C4
+  // wide step). gups_n: [s] chunks listed in segment s (past gups_seg a
+  // streamer applies its chunk itself), [kGupsShards] finished k_gups_apply
+  // workgroups. gups_stat: per k_gups_apply workgroup, updates generated and
+  // atomics issued (an update whose XOR operand is 0 changes no word and is
+  // not issued; same-word updates of one wave are combined).
+  uint64_t* gups_list;
+  unsigned int* gups_n;
+  const uint64_t* gups_jump;
+  unsigned long long* gups_stat;
+  uint32_t gups_seg, gups_l, gups_parts;
+  int32_t gups_type;
 };
+constexpr uint32_t kGupsShards = 64;
 constexpr uint32_t kShards = 32;
 // landed records that make a zone hot (hot_dev.h). k_step consumes a prepared
 // zone's counts only on its scratch path, so a hot zone must never fit the
@@ -393,11 +414,10 @@ __device__ __forceinline__ void reducible_apply_local(uint32_t to, uint32_t beh,
         (unsigned long long)arg);
       break;
     case GPU_ACTOR_HT_GUPS_UPDATER: {
-      // t[d & m] ^= d; d == 0 is the identity (send_updater)
+      // t[d & m] ^= d
       const uint64_t k = arg & (T.params[0] - 1);
-      if(arg != 0)
-        atomicXor(reinterpret_cast<unsigned long long*>(&T.state[k * T.lcount + li]),
-          (unsigned long long)arg);
+      atomicXor(reinterpret_cast<unsigned long long*>(&T.state[k * T.lcount + li]),
+        (unsigned long long)arg);
       break;
     }
     default:
@@ -637,17 +657,34 @@ __device__ __forceinline__ void send_updater(A& a, uint32_t to, uint64_t d)
     a.rc_state = T.state;
     a.rc_mask = T.params[0] - 1;
   }
-  // gups_basic Updater.apply: t[d & (size - 1)] ^= d. An update with d == 0
-  // is the identity and changes no word: it is counted, not issued. (The
-  // reference's PolyRand._seed drops bit 63 of each squaring — its m2 table
-  // has 63 entries — and maps 1/16 of the streamers of C4's wide config to
-  // the seed 0, whose stream stays 0: 65,535 streamers XOR 0 into word 0 of
-  // updater 0 at the same time, one memory-side atomic queue for 1/16 of the
-  // updates; scripts/ubench_gups2.hip, profiles/r05b_ubench_gups2.txt.)
+  // gups_basic Updater.apply: t[d & (size - 1)] ^= d, every update issued
+  // (the streamers' chunks on one rank go through k_gups_apply instead)
   const uint32_t li = rdiv(to) - a.rc_lfirst;
-  if(d != 0)
-    atomicXor(reinterpret_cast<unsigned long long*>(&a.rc_state[(d & a.rc_mask) * a.rc_lcount + li]),
-      (unsigned long long)d);
+  atomicXor(reinterpret_cast<unsigned long long*>(&a.rc_state[(d & a.rc_mask) * a.rc_lcount + li]),
+    (unsigned long long)d);
+}
+
+// A GUPS streamer's chunk handed to k_gups_apply: its PolyRand state before
+// the chunk listed (one list atomic per wave, on the wave's segment), the
+// chunk's updates counted as sent and applied here. False when the segment is
+// full: the streamer applies the chunk itself.
+template <class A>
+__device__ __forceinline__ bool gups_defer(A& a, uint64_t last, uint64_t chunk, uint32_t ubase)
+{
+  const uint64_t m = __ballot(1);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const uint32_t sh = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kGupsShards - 1u);
+  unsigned int base = 0;
+  if(below == 0) base = atomicAdd(&c_eng.gups_n[sh], (unsigned int)__popcll(m));
+  base = __builtin_amdgcn_readfirstlane(base);
+  const unsigned int i = base + below;
+  if(i >= c_eng.gups_seg) return false;
+  c_eng.gups_list[(size_t)sh * c_eng.gups_seg + i] = last;
+  a.sent += (uint32_t)chunk;
+  a.applied += (uint32_t)chunk;
+  if(a.applied_type < 0) a.applied_type = type_of_global(ubase);
+  return true;
 }
 
 // ---- handler tables --------------------------------------------------------
@@ -766,11 +803,15 @@ __device__ __forceinline__ void handle(HtTag<GPU_ACTOR_HT_GUPS_STREAMER>, const 
   const uint64_t chunk = T.params[0], shift = T.params[1], mask = T.params[2];
   const uint32_t ubase = (uint32_t)T.params[3];
   uint64_t last = s[0];
-  for(uint64_t c = 0; c < chunk; ++c)
-  {
-    const uint64_t d = polyrand_next(last);
-    send_updater(a, ubase + (uint32_t)((d >> shift) & mask), d);
-  }
+  // one rank: the chunk goes to k_gups_apply, the state jumps past it
+  if(a.type == c_eng.gups_type && gups_defer(a, last, chunk, ubase))
+    last = polyrand_mulmod(last, c_eng.gups_jump[c_eng.gups_parts]);
+  else
+    for(uint64_t c = 0; c < chunk; ++c)
+    {
+      const uint64_t d = polyrand_next(last);
+      send_updater(a, ubase + (uint32_t)((d >> shift) & mask), d);
+    }
   s[0] = last;
   if(arg > 0)
     send_serial(a, a.self, GPU_ACTOR_GUPS_APPLY, arg - 1);

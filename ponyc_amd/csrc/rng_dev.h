@@ -78,6 +78,34 @@ __device__ __forceinline__ uint64_t polyrand_next(uint64_t& last)
   return last;
 }
 
+// PolyRand's step is a product by x in GF(2)[x] / (x^64 + x^2 + x + 1), so n
+// steps are one product by x^n: a * b mod that polynomial, b's bits high to
+// low (the jump-ahead _seed makes through its squaring table, exact here in
+// all 64 bits).
+__host__ __device__ inline uint64_t polyrand_mulmod(uint64_t a, uint64_t b)
+{
+  uint64_t r = 0;
+  for(int i = 63; i >= 0; --i)
+  {
+    r = (r << 1) ^ ((int64_t)r < 0 ? 7ULL : 0ULL);
+    if((b >> i) & 1) r ^= a;
+  }
+  return r;
+}
+
+// x^n mod the PolyRand polynomial (square and multiply)
+__host__ __device__ inline uint64_t polyrand_xpow(uint64_t n)
+{
+  uint64_t r = 1, b = 2;
+  while(n)
+  {
+    if(n & 1) r = polyrand_mulmod(r, b);
+    b = polyrand_mulmod(b, b);
+    n >>= 1;
+  }
+  return r;
+}
+
 // PolyRand._seed: x^n style jump through the squaring table m2 (63 entries;
 // the reference's m2(63) read is out of bounds and skipped inside `try`).
 __device__ inline uint64_t polyrand_seeded(uint64_t seed)

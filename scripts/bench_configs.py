@@ -3,7 +3,9 @@ only, as the task contract asks; this reports the others for DESIGN.md).
 
 Each workload is built with ponyc_amd.workloads at its BASELINE size and run
 to quiescence with gpu_actor_run; rate = delivered messages / wall time of the
-run (host sends done before the clock starts). One JSON line per config.
+run (host sends done before the clock starts), from the second of two runs on
+fresh engines (the first's time is reported beside it: it also loads the
+kernels' code objects). One JSON line per config.
 With --cpu, the reference runtime (oracle/_ref/harness_*, libponyrt built
 from the reference sources) runs the same config on the host's cores
 (--ponymaxthreads = every usable physical core, bench.py's host_cores rule,
@@ -43,6 +45,12 @@ CONFIGS = {
     # C4 at its stated size: 2^30-word table as 8 shards, 2^32 updates
     # (2^18 streamers x 4096 x (3 + 1)); checked in tests/test_gpu_fullsize.py
     "c4_gups_2p32": (lambda e: W.gups(e, 30, 8, 1 << 18, 4096, 3), {}),
+    # the two C4 shapes with every streamer applying its own chunk (no
+    # k_gups_apply: every update issued as its own atomic, none combined or
+    # skipped) — the comparison ADVICE r05 asks for
+    "c4_gups_own": (lambda e: W.gups(e, 24, 8, 64, 1024, 100), {}, {"PONYC_AMD_GUPS_DEFER": "0"}),
+    "c4_gups_wide_own": (lambda e: W.gups(e, 30, 8, 1 << 20, 16, 8), {},
+                         {"PONYC_AMD_GUPS_DEFER": "0"}),
     # C5, one GPU's share: 8M actors, token ring + 4 random pings each, 16 hops
     "c5_storm_8m": (lambda e: W.storm(e, 8 * M, 4, 16), {}),
     # C5 at its stated 1000 steps (41.9 G messages)
@@ -81,22 +89,42 @@ def main():
     args = sys.argv[1:]
     with_cpu = "--cpu" in args
     names = [a for a in args if a != "--cpu"] or [n for n in CONFIGS if not n.endswith("_1000")
-                                                   and n != "c4_gups_2p32"]
+                                                   and n != "c4_gups_2p32" and not n.endswith("_own")]
     for name in names:
-        setup, kw = CONFIGS[name]
-        e = Engine(**kw)
-        setup(e)
-        e.sync()
-        t0 = time.perf_counter()
-        steps = e.run()
-        e.sync()
-        secs = time.perf_counter() - t0
-        c = e.counts()
-        e.shutdown()
-        print(json.dumps({"config": name, "steps": steps, "delivered": c["delivered"],
-                          "seconds": round(secs, 4), "msgs_per_s": round(c["delivered"] / secs, 1),
-                          "dropped": c["dropped"],
-                          "cpu_ref": cpu_ref(name) if with_cpu else None}), flush=True)
+        setup, kw, *env = CONFIGS[name]
+        saved = {k: os.environ.get(k) for k in (env[0] if env else {})}
+        os.environ.update(env[0] if env else {})
+        # twice, on a fresh engine each time: the first run in a process also
+        # loads its kernels' code objects (lazily, at their first launch)
+        first = None
+        for _ in range(2):
+            e = Engine(**kw)
+            setup(e)
+            e.sync()
+            t0 = time.perf_counter()
+            steps = e.run()
+            e.sync()
+            secs = time.perf_counter() - t0
+            c = e.counts()
+            d = e.debug_info()
+            e.shutdown()
+            first = secs if first is None else first
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        line = {"config": name, "steps": steps, "delivered": c["delivered"],
+                "seconds": round(secs, 4), "msgs_per_s": round(c["delivered"] / secs, 1),
+                "first_run_seconds": round(first, 4),
+                "dropped": c["dropped"], "env": env[0] if env else None,
+                "cpu_ref": cpu_ref(name) if with_cpu else None}
+        if d["gups_updates"]:
+            # k_gups_apply's updates and the atomics it issued for them (the
+            # rest were combined with a same-word update of their wave, or
+            # were XORs of 0)
+            line["gups_apply"] = {"updates": d["gups_updates"], "atomics": d["gups_atomics"]}
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -75,6 +75,30 @@ def test_gups_many_streamers(engine_factory, oracle):
     _assert_same(g, o)
 
 
+@pytest.mark.parametrize("defer", ["1", "0"])
+@pytest.mark.parametrize("logtable,updaters,streamers,chunk,iterate",
+                         [(16, 8, 4, 1024, 10), (4, 2, 256, 1024, 3), (12, 4, 64, 100, 5),
+                          (10, 1, 1000, 16, 4), (8, 4, 3, 4096, 2)])
+def test_gups_chunks(engine_factory, oracle, monkeypatch, defer, logtable, updaters, streamers,
+                     chunk, iterate):
+    """C4's chunks on one rank go to k_gups_apply (engine.hip): lane-parallel
+    PolyRand by jump-ahead, same-word updates of a wave combined, XORs of 0 not
+    issued; PONYC_AMD_GUPS_DEFER=0 has every streamer apply its own chunk,
+    every update issued. Both bit-exact against the oracle. (4, 2, ...) is the
+    skewed case: 2^20 updates on 16 words."""
+    monkeypatch.setenv("PONYC_AMD_GUPS_DEFER", defer)
+    g, o = _both(engine_factory, oracle,
+                 lambda e: W.gups(e, logtable, updaters, streamers, chunk, iterate), W.gups_result)
+    _assert_same(g, o)
+    d = g[1]["debug"]
+    n = streamers * chunk * (iterate + 1)
+    if defer == "1":
+        assert d["gups_updates"] == n
+        assert 0 < d["gups_atomics"] <= n
+    else:
+        assert d["gups_updates"] == 0
+
+
 def test_storm(engine_factory, oracle):
     g, o = _both(engine_factory, oracle, lambda e: W.storm(e, 3000, 4, 12), lambda e, w: e.state_read(w["type"]))
     _assert_same(g, o)
