@@ -374,6 +374,13 @@ struct Engine {
   uint32_t xspill_cap = 0;
   std::vector<unsigned long long> h_xcount, h_xrecv;   // host transport
   uint64_t remote_total = 0;
+  // peer writes (PONYC_AMD_PEER_WRITE=1, EngDev::peer_write): this rank's
+  // inbox [R][xcap] (segment p: peer p's records, stored by peer p's k_step),
+  // every peer's inbox mapped over IPC, and a small collective scratch
+  bool peer_write = false;
+  XRec* d_pin = nullptr;
+  XRec* peer_ptr[kMaxRanks] = {};
+  unsigned long long* d_hx = nullptr;      // [1 + R]
   // host transport (gpu_actor_set_transport)
   gpu_actor_alltoallv_fn xp_a2a = nullptr;
   gpu_actor_allreduce_fn xp_ar = nullptr;
@@ -672,6 +679,10 @@ int upload_types()
     e.hot_bar = h;
   }
   e.xout = g.d_xout; e.xcount = g.d_xcount; e.xcap = g.xcap;
+  e.peer_write = g.peer_write ? 1u : 0u;
+  for(uint32_t p = 0; p < R() && p < kMaxRanks; ++p)
+    e.xdst[p] = g.peer_write ? (g.peer_ptr[p] ? g.peer_ptr[p] + (size_t)rank() * g.xcap : nullptr)
+                             : (g.d_xout ? g.d_xout + (size_t)p * g.xcap : nullptr);
   e.seq_max = R() > 1 ? kXSeqMax : kSeqMax;
   e.dbg = g.d_dbg;
   e.spawn_key = g.d_skey[0]; e.spawn_arg = g.d_sarg[0];
@@ -1272,7 +1283,7 @@ __global__ void __launch_bounds__(kBlock) k_xspill_place(uint32_t n)
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if(i >= n) return;
   const XSpillRec r = c_eng.xspill[i];
-  c_eng.xout[(size_t)r.peer * c_eng.xcap + r.pos] = r.rec;
+  xrec_put(c_eng.xdst[r.peer] + r.pos, r.rec);
 }
 
 int alloc_xspill(uint32_t cap)
@@ -1289,8 +1300,10 @@ int alloc_xspill(uint32_t cap)
 // peer segments grow (kept records are copied to the new stride) and the
 // spilled records go to their reserved positions; xin grows. Local decisions
 // only: each side sizes its own buffers.
+int peer_room(uint64_t max_send, uint64_t xs);
 int exchange_room(uint64_t max_send, uint64_t total_recv, uint64_t xs)
 {
+  if(g.peer_write) return peer_room(max_send, xs);
   const bool lost = xs > g.xspill_cap;     // k_xprep clipped the counts to xcap
   if(max_send > g.xcap || lost)
   {
@@ -1513,6 +1526,129 @@ uint64_t trig_live_bytes()
   return std::min<uint64_t>(g.trig_bytes, (zones * zone_actors() * R() + 7) & ~7ull);
 }
 
+// Peer writes: map every peer's inbox (hipIpcGetMemHandle / hipIpcOpenMemHandle),
+// the handles gathered word by word over the engine's collectives (RCCL or the
+// host transport). Collective: every rank calls it at the same point.
+void peer_close()
+{
+  for(uint32_t p = 0; p < kMaxRanks; ++p)
+  {
+    if(g.peer_ptr[p] && p != rank()) (void)hipIpcCloseMemHandle(g.peer_ptr[p]);
+    g.peer_ptr[p] = nullptr;
+  }
+}
+
+int peer_open()
+{
+  hipIpcMemHandle_t h;
+  HIPCK(hipIpcGetMemHandle(&h, g.d_pin));
+  static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "IPC handle in u64 words");
+  constexpr uint32_t kW = sizeof(hipIpcMemHandle_t) / 8;
+  const uint32_t n = R();
+  std::vector<unsigned long long> all((size_t)kW * n), got(n);
+  for(uint32_t w = 0; w < kW; ++w)
+  {
+    unsigned long long v;
+    memcpy(&v, reinterpret_cast<const char*>(&h) + 8 * w, 8);
+    HIPCK(hipMemcpyAsync(g.d_hx, &v, 8, hipMemcpyHostToDevice, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    const int rc = xc_allgather_u64(g.d_hx, g.d_hx + 1);
+    if(rc) return rc;
+    HIPCK(hipMemcpyAsync(got.data(), g.d_hx + 1, n * 8, hipMemcpyDeviceToHost, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    for(uint32_t p = 0; p < n; ++p) all[(size_t)p * kW + w] = got[p];
+  }
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    if(p == rank())
+    {
+      g.peer_ptr[p] = g.d_pin;
+      continue;
+    }
+    hipIpcMemHandle_t hp;
+    memcpy(&hp, &all[(size_t)p * kW], sizeof(hp));
+    void* ptr = nullptr;
+    HIPCK(hipIpcOpenMemHandle(&ptr, hp, hipIpcMemLazyEnablePeerAccess));
+    g.peer_ptr[p] = static_cast<XRec*>(ptr);
+  }
+  return 0;
+}
+
+// exchange_room with peer writes: a segment lives in its receiver's inbox, so
+// the segments grow on every rank alike — to the largest size any rank needs
+// (one gather of each rank's need and whether it kept records in its exchange
+// spill list), the kept records moved to the new stride by each inbox's owner,
+// the inboxes mapped again; then the spilled records go to their peers, and
+// when any rank placed some, one more collective orders those stores before
+// every owner's k_xinject.
+int peer_room(uint64_t max_send, uint64_t xs)
+{
+  const bool lost = xs > g.xspill_cap;     // k_xprep clipped the counts to xcap
+  uint64_t want = 0;
+  if(max_send > g.xcap || lost)
+  {
+    want = std::max<uint64_t>(2ull * g.xcap, max_send + max_send / 2);
+    want = std::min<uint64_t>((want + 63) & ~63ull, 0x40000000ull);
+  }
+  const uint32_t n = R();
+  const unsigned long long mine = want << 1 | (xs ? 1ull : 0ull);
+  HIPCK(hipMemcpyAsync(g.d_hx, &mine, 8, hipMemcpyHostToDevice, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  int rc = xc_allgather_u64(g.d_hx, g.d_hx + 1);
+  if(rc) return rc;
+  std::vector<unsigned long long> all(n);
+  HIPCK(hipMemcpyAsync(all.data(), g.d_hx + 1, n * 8, hipMemcpyDeviceToHost, g.stream));
+  HIPCK(hipStreamSynchronize(g.stream));
+  uint64_t cap = g.xcap;
+  bool any_xs = false;
+  for(uint32_t p = 0; p < n; ++p)
+  {
+    cap = std::max<uint64_t>(cap, all[p] >> 1);
+    any_xs |= (all[p] & 1ull) != 0;
+  }
+  if(cap > g.xcap)
+  {
+    XRec* nx = nullptr;
+    HIPCK(hipMalloc(&nx, (size_t)n * cap * sizeof(XRec)));
+    HIPCK(hipMemcpy2DAsync(nx, cap * sizeof(XRec), g.d_pin, (size_t)g.xcap * sizeof(XRec),
+      (size_t)g.xcap * sizeof(XRec), n, hipMemcpyDeviceToDevice, g.stream));
+    HIPCK(hipStreamSynchronize(g.stream));
+    peer_close();
+    HIPCK(hipFree(g.d_pin));
+    g.d_pin = nx;
+    g.xcap = (uint32_t)cap;
+    rc = peer_open();
+    if(rc) return rc;
+    rc = upload_types();
+    if(rc) return rc;
+  }
+  if(xs)
+  {
+    if(!lost)
+    {
+      hipLaunchKernelGGL(k_xspill_place, dim3(blocks_for(xs)), dim3(kBlock), 0, g.stream,
+        (uint32_t)xs);
+      HIPCK(hipGetLastError());
+    }
+    HIPCK(hipMemsetAsync(g.d_xspill_n, 0, sizeof(unsigned int), g.stream));
+    if(xs > g.xspill_cap / 2)
+    {
+      HIPCK(hipStreamSynchronize(g.stream));
+      rc = alloc_xspill((uint32_t)std::min<uint64_t>(4ull * std::max<uint64_t>(xs, g.xspill_cap),
+        1ull << 27));
+      if(rc) return rc;
+      rc = upload_types();
+      if(rc) return rc;
+    }
+  }
+  if(any_xs)
+  {
+    rc = xc_allreduce_sum(g.d_hx, g.d_hx, 1, XC_U64);
+    if(rc) return rc;
+  }
+  return 0;
+}
+
 int exchange_step(uint32_t step_sidx)
 {
   const uint32_t n = R(), land_par = g.par, tslot = (step_sidx + 1) % 3;
@@ -1553,22 +1689,28 @@ int exchange_step(uint32_t step_sidx)
   if(rc) return rc;
   // the records: each peer's segment of xout to it, its records into xin in
   // rank order (k_xinject tells the sender of a record by its segment)
-  std::vector<XcPeer> pp(n);
-  for(uint32_t p = 0; p < n; ++p)
+  // (with peer writes they are in this rank's inbox already: every peer's
+  // k_step stored them there before its counts went out)
+  if(!g.peer_write)
   {
-    if(p == rank()) continue;
-    pp[p].d_send = g.d_xout + (size_t)p * g.xcap;
-    pp[p].send = g.h_xc[p] * sizeof(XRec);
-    pp[p].d_recv = g.d_xin + roff[p];
-    pp[p].recv = g.h_xc[n + p] * sizeof(XRec);
+    std::vector<XcPeer> pp(n);
+    for(uint32_t p = 0; p < n; ++p)
+    {
+      if(p == rank()) continue;
+      pp[p].d_send = g.d_xout + (size_t)p * g.xcap;
+      pp[p].send = g.h_xc[p] * sizeof(XRec);
+      pp[p].d_recv = g.d_xin + roff[p];
+      pp[p].recv = g.h_xc[n + p] * sizeof(XRec);
+    }
+    rc = xc_sendrecv(pp);
+    if(rc) return rc;
   }
-  rc = xc_sendrecv(pp);
-  if(rc) return rc;
   g.remote_total += total;
   if(total)
   {
     hipLaunchKernelGGL(k_xinject, dim3(blocks_for(total, kLandRecs)), dim3(kLandThreads), 0, g.stream,
-      (const XRec*)g.d_xin, total, land_par, (const unsigned long long*)g.d_xrecv);
+      (const XRec*)(g.peer_write ? g.d_pin : g.d_xin), total, land_par,
+      (const unsigned long long*)g.d_xrecv, g.peer_write ? (uint64_t)g.xcap : 0ull);
     HIPCK(hipGetLastError());
   }
   HIPCK(hipMemsetAsync(g.d_xcount, 0, n * sizeof(unsigned long long), g.stream));
@@ -2058,6 +2200,9 @@ void free_all()
   if(g.d_msgs) (void)hipFree(g.d_msgs);
   if(g.d_xout) (void)hipFree(g.d_xout);
   if(g.d_xin) (void)hipFree(g.d_xin);
+  peer_close();
+  if(g.d_pin) (void)hipFree(g.d_pin);
+  if(g.d_hx) (void)hipFree(g.d_hx);
   if(g.d_xspill) (void)hipFree(g.d_xspill);
   if(g.d_xspill_n) (void)hipFree(g.d_xspill_n);
   if(g.d_xc) (void)hipFree(g.d_xc);
@@ -2253,9 +2398,21 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
       // its staging grows on demand (stage_room)
       if(!g.xp_a2a || !g.xp_ar) return GPU_ACTOR_EINVAL;
     }
-    HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
-    HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
-    g.xin_cap = (uint64_t)R() * g.xcap;
+    {
+      const char* pw = getenv("PONYC_AMD_PEER_WRITE");
+      g.peer_write = pw && atoi(pw) != 0;
+    }
+    if(g.peer_write)
+    {
+      HIPCK(hipMalloc(&g.d_pin, (size_t)R() * g.xcap * sizeof(XRec)));
+      HIPCK(hipMalloc(&g.d_hx, (1 + R()) * sizeof(unsigned long long)));
+    }
+    else
+    {
+      HIPCK(hipMalloc(&g.d_xout, (size_t)R() * g.xcap * sizeof(XRec)));
+      HIPCK(hipMalloc(&g.d_xin, (size_t)R() * g.xcap * sizeof(XRec)));
+      g.xin_cap = (uint64_t)R() * g.xcap;
+    }
     HIPCK(hipMalloc(&g.d_xspill_n, sizeof(unsigned int)));
     HIPCK(hipMemsetAsync(g.d_xspill_n, 0, sizeof(unsigned int), g.stream));
     {
@@ -2269,6 +2426,12 @@ GPU_ACTOR_API int gpu_actor_init(const gpu_actor_config_t* cfg)
     g.d_xrecv = g.d_xc + R();
     g.h_xcount.assign(R(), 0);
     g.h_xrecv.assign(R(), 0);
+    if(g.peer_write)
+    {
+      HIPCK(hipStreamSynchronize(g.stream));
+      const int prc = peer_open();
+      if(prc) return prc;
+    }
   }
   g.init = true;
   int rc = upload_types();
@@ -2356,7 +2519,8 @@ GPU_ACTOR_API int gpu_actor_shutdown(void)
   g.h_msgs = nullptr; g.h_msgs_cap = 0; g.d_msgs = nullptr; g.d_msgs_cap = 0;
   g.host_seq = 0; g.steps_total = 0; g.sticky = 0; g.ev.clear(); g.last_drain_ms = 0;
   g.deferred.clear();
-  g.comm = nullptr; g.d_xout = g.d_xin = nullptr; g.d_xcount = g.d_xrecv = nullptr;
+  g.comm = nullptr; g.d_xout = g.d_xin = nullptr;
+  g.d_pin = nullptr; g.d_hx = nullptr; g.peer_write = false; g.d_xcount = g.d_xrecv = nullptr;
   g.d_xc = nullptr; g.h_xc = nullptr; g.d_spill_flag = nullptr;
   g.xcap = 0; g.remote_total = 0; g.stream = nullptr;
   g.xin_cap = 0; g.d_xspill = nullptr; g.d_xspill_n = nullptr; g.xspill_cap = 0;
@@ -3073,10 +3237,11 @@ GPU_ACTOR_API int gpu_actor_debug_info(uint64_t* out, uint64_t n)
     HIPCK(hipStreamSynchronize(g.stream));
     for(uint32_t b = 0; b < kGupsBlocks; ++b) { gu[0] += st[b]; gu[1] += st[kGupsBlocks + b]; }
   }
-  const uint64_t v[16] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
+  // + [16] whether cross-rank records go straight into the peers' inboxes
+  const uint64_t v[17] = {g.fixups, g.sparse_launches, g.sparse_steps, g.zone_records, g.spill_cap,
                           g.n_zones, tn[0], tn[1], tn[2], g.zbits, hb[3], g.hot_on ? 1u : 0u,
-                          g.jit_used ? 1u : 0u, g.jit_builds, gu[0], gu[1]};
-  for(uint64_t i = 0; i < n && i < 16; ++i) out[i] = v[i];
+                          g.jit_used ? 1u : 0u, g.jit_builds, gu[0], gu[1], g.peer_write ? 1u : 0u};
+  for(uint64_t i = 0; i < n && i < 17; ++i) out[i] = v[i];
   return 0;
 }
 

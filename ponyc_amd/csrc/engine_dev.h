@@ -153,7 +153,7 @@ struct EngDev {
   ORec* O;                        // zone z: [zoff[z], zoff[z] + zcapz[z])
   unsigned long long* stats;
   unsigned long long* pend;       // per-step pending counters
-  XRec*  xout;                    // [nranks][xcap]
+  XRec*  xout;                    // [nranks][xcap] (unused with peer_write: xdst)
   unsigned long long* xcount;     // [nranks]
   uint32_t xcap;
   uint32_t seq_max;               // kSeqMax, or kXSeqMax with n_ranks > 1
@@ -252,6 +252,13 @@ struct EngDev {
   unsigned long long* gups_stat;
   uint32_t gups_seg, gups_l, gups_parts;
   int32_t gups_type;
+  // cross-rank records for peer p go to xdst[p][pos], pos < xcap: this rank's
+  // segment p of xout, or with peer_write (engine.hip peer_open) this rank's
+  // segment of peer p's inbox, mapped over IPC, so that the records cross
+  // xGMI as k_step stores them and only the counts go through the collectives
+  // (their stores, and the owner's loads, at system scope: xrec_put/xrec_get)
+  XRec* xdst[kMaxRanks];
+  uint32_t peer_write, pad9;
 };
 constexpr uint32_t kGupsShards = 64;
 constexpr uint32_t kShards = 32;
@@ -454,11 +461,39 @@ __device__ __forceinline__ void spill_rec(uint32_t p, uint32_t kind, uint32_t z,
 // Store cross-rank record x at reserved position pos of peer segment `peer`;
 // past the segment's capacity it goes to the exchange spill list (lost, and
 // counted, only when that list is full too). Returns 1 if it was lost.
+// A cross-rank record's store into its segment (EngDev::xdst) and its load by
+// k_xinject: with peer_write the segment is another GPU's memory, written by
+// this GPU's stores over xGMI and read by its owner while neither L2 may hold
+// a copy, so both sides go to memory (system scope); plain otherwise.
+__device__ __forceinline__ void xrec_put(XRec* d, const XRec& x)
+{
+  if(c_eng.peer_write)
+  {
+    uint64_t* q = reinterpret_cast<uint64_t*>(d);
+    __hip_atomic_store(q, (uint64_t)x.w1 << 32 | x.w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, x.arg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  else
+    *d = x;
+}
+
+__device__ __forceinline__ XRec xrec_get(const XRec* s)
+{
+  if(!c_eng.peer_write) return *s;
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(s);
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  XRec x;
+  x.w0 = (uint32_t)a;
+  x.w1 = (uint32_t)(a >> 32);
+  x.arg = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return x;
+}
+
 __device__ __forceinline__ uint32_t xout_store(uint32_t peer, uint32_t pos, const XRec& x)
 {
   if(pos < c_eng.xcap)
   {
-    c_eng.xout[(size_t)peer * c_eng.xcap + pos] = x;
+    xrec_put(c_eng.xdst[peer] + pos, x);
     return 0;
   }
   const unsigned int i = atomicAdd(c_eng.xspill_n, 1u);

@@ -2911,10 +2911,12 @@ __global__ void __launch_bounds__(kLandThreads) k_inject(const gpu_msg_t* msgs, 
 }
 
 // Records received from other ranks: `in` holds each peer's records in rank
-// order, rcnt[p] of them from peer p; the sender's rank of a record is the
-// segment it lies in.
+// order, rcnt[p] of them from peer p — back to back (stride 0: received by
+// the collectives), or peer p's at in + p * stride (the inbox peers stored
+// into, EngDev::peer_write); the sender's rank of a record is the segment it
+// lies in.
 __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64_t n, uint32_t cur,
-  const unsigned long long* rcnt)
+  const unsigned long long* rcnt, uint64_t stride)
 {
   __shared__ uint32_t s_hist[kMaxZones];
   __shared__ uint32_t s_base[kMaxZones];
@@ -2940,10 +2942,10 @@ __global__ void __launch_bounds__(kLandThreads) k_xinject(const XRec* in, uint64
     r[u].valid = false;
     if(i < n)
     {
-      const XRec x = in[i];
       uint32_t src = 0;
       for(uint32_t p = 1; p < R; ++p)
         if(i >= s_roff[p]) src = p;
+      const XRec x = stride ? xrec_get(in + src * stride + (i - s_roff[src])) : in[i];
       const uint32_t seq = (x.w0 >> 27) << 9 | (x.w1 >> 23);
       const uint32_t beh = (x.w0 >> 23) & 0xFu;
       const uint32_t to = (x.w0 & 0x7FFFFFu) * R + me;

@@ -377,7 +377,7 @@ class Engine:
         """Engine internals (diagnostic export, not in include/gpu_actor.h)."""
         keys = ["fixups", "sparse_launches", "sparse_steps", "zone_records", "spill_cap", "zones",
                 "trig_n0", "trig_n1", "trig_n2", "zone_bits", "hot_missed", "hot_on", "jit",
-                "jit_builds", "gups_updates", "gups_atomics"]
+                "jit_builds", "gups_updates", "gups_atomics", "peer_write"]
         out = (ctypes.c_uint64 * len(keys))()
         fn = self.lib.gpu_actor_debug_info
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]

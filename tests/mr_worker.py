@@ -107,6 +107,7 @@ def main():
     w = setup(eng)
     steps = drive(eng, mode)
     c = eng.counts()
+    peer_write = eng.debug_info()["peer_write"]
     res = result(GlobalView(eng), w)
     eng.shutdown()
     if rank == 0:
@@ -125,7 +126,7 @@ def main():
             "sent": [c["sent"], co["sent"]],
             "pending": [c["pending"], co["pending"]],
             "by_type": c["delivered_by_type"] == co["delivered_by_type"],
-            "dropped": c["dropped"], "remote": c["remote"],
+            "dropped": c["dropped"], "remote": c["remote"], "peer_write": peer_write,
         }
         print("MR_RESULT " + json.dumps(out), flush=True)
     dist.barrier()
