@@ -2767,14 +2767,20 @@ bool sparse_ok()
 int run_sparse(uint64_t max_steps, SparseCtl& out)
 {
   g.dev_epoch++;
-  bool prog = false;
-  for(const HostType& t : g.types) prog |= t.created && t.ht == GPU_ACTOR_HT_PROGRAM;
-  if(prog)
-    hipLaunchKernelGGL(k_sparse<true>, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
-      (unsigned long long)max_steps, g.d_ctl, g.sidx);
-  else
-    hipLaunchKernelGGL(k_sparse<false>, dim3(1), dim3(kSpThreads), 0, g.stream, g.par,
-      (unsigned long long)max_steps, g.d_ctl, g.sidx);
+  bool prog = false, gups = false;
+  for(const HostType& t : g.types)
+  {
+    prog |= t.created && t.ht == GPU_ACTOR_HT_PROGRAM;
+    gups |= t.created && t.ht == GPU_ACTOR_HT_GUPS_STREAMER;
+  }
+#define GPA_SPARSE_LAUNCH(P, G)                                                         \
+  hipLaunchKernelGGL((k_sparse<P, G>), dim3(1), dim3(kSpThreads), 0, g.stream, g.par,   \
+    (unsigned long long)max_steps, g.d_ctl, g.sidx)
+  if(prog && gups) GPA_SPARSE_LAUNCH(true, true);
+  else if(prog) GPA_SPARSE_LAUNCH(true, false);
+  else if(gups) GPA_SPARSE_LAUNCH(false, true);
+  else GPA_SPARSE_LAUNCH(false, false);
+#undef GPA_SPARSE_LAUNCH
   HIPCK(hipGetLastError());
   {
     // the chunks its supersteps listed (2^16 or more per segment)

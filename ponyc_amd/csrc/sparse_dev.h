@@ -127,8 +127,11 @@ __device__ __forceinline__ void sp_drain(const TypeDev& T, SparseCtx& a, const S
 
 // kProg: the engine holds program types (GPU_ACTOR_HT_PROGRAM); their
 // interpreter is compiled into a k_sparse of its own (in the one kernel it
-// cost the compiled ring 13 %: 41.2 -> 35.7 M msgs/s, profiles/r05p4_sparse_program_ab.txt)
-template <bool kProg>
+// cost the compiled ring 13 %: 41.2 -> 35.7 M msgs/s, profiles/r05p4_sparse_program_ab.txt).
+// kGups: the same for the GUPS streamer, whose chunk listing and GF(2) jump
+// (k_gups_apply) cost the ring 10 % in the one kernel (40.8 -> 36.7 M msgs/s,
+// profiles/r06_ring_ab.txt).
+template <bool kProg, bool kGups>
 __device__ __forceinline__ void sp_dispatch(const TypeDev& Tref, SparseCtx& a, const SpList& S,
   uint32_t i, uint32_t g, uint32_t L)
 {
@@ -141,7 +144,9 @@ __device__ __forceinline__ void sp_dispatch(const TypeDev& Tref, SparseCtx& a, c
     SPCASE(GPU_ACTOR_HT_PINGER)
     SPCASE(GPU_ACTOR_HT_PINGER_DET)
     SPCASE(GPU_ACTOR_HT_FANIN_SENDER)
-    SPCASE(GPU_ACTOR_HT_GUPS_STREAMER)
+    case GPU_ACTOR_HT_GUPS_STREAMER:
+      if constexpr(kGups) sp_drain<GPU_ACTOR_HT_GUPS_STREAMER>(T, a, S, i, g);
+      break;
     SPCASE(GPU_ACTOR_HT_STORM)
     SPCASE(GPU_ACTOR_HT_FIFO_SRC)
     SPCASE(GPU_ACTOR_HT_FIFO_SINK)
@@ -179,7 +184,7 @@ __device__ __forceinline__ uint32_t sp_block_excl_scan(uint32_t v, uint32_t* s_t
 
 // Runs up to max_steps supersteps (0: no limit) starting from the records in
 // landing[cur]; R == 1 and no spawning types (the host checks).
-template <bool kProg>
+template <bool kProg, bool kGups>
 __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned long long max_steps,
   SparseCtl* ctl, uint32_t sidx)
 {
@@ -208,6 +213,7 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
     // reducible types never run; spawning and yielding ones need the zone path
     s_tinfo[tid].flags = (T.reducible || T.ht == GPU_ACTOR_HT_SPREADER ||
                           (T.ht == GPU_ACTOR_HT_PROGRAM && (!kProg || (T.prog_pad & 1u))) ||
+                          (T.ht == GPU_ACTOR_HT_GUPS_STREAMER && !kGups) ||
                           (T.ht == GPU_ACTOR_HT_FIFO_SINK && T.params[1] != 0)) ? kSpNoRun : 0u;
   }
   if(tid == 0) { sp_cnt[0] = 0; sp_cnt[1] = 0; s_over = 0; }
@@ -419,8 +425,8 @@ __global__ void __launch_bounds__(kSpThreads) k_sparse(uint32_t cur, unsigned lo
       // the usual case, one type for every run of the wave: its fields come
       // through scalar loads instead of a per-lane copy from constant memory
       const int tu = __builtin_amdgcn_readfirstlane(t);
-      if(__ballot(t != tu) == 0ull) sp_dispatch<kProg>(c_types[tu], a, Sr, h_r, h_g, L);
-      else sp_dispatch<kProg>(c_types[t], a, Sr, h_r, h_g, L);
+      if(__ballot(t != tu) == 0ull) sp_dispatch<kProg, kGups>(c_types[tu], a, Sr, h_r, h_g, L);
+      else sp_dispatch<kProg, kGups>(c_types[t], a, Sr, h_r, h_g, L);
       delivered += h_g;
       active += 1;
       sent += a.sent;
