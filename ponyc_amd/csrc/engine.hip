@@ -612,7 +612,14 @@ int gups_setup(EngDev& e)
   }
   e.gups_list = g.d_gups_list; e.gups_n = g.d_gups_n; e.gups_jump = g.d_gups_jump;
   e.gups_stat = g.d_gups_stat;
-  e.gups_seg = g.gups_cap / kGupsShards; e.gups_l = (uint32_t)L; e.gups_parts = (uint32_t)parts;
+  e.gups_seg = g.gups_cap / kGupsShards;
+  {
+    // (tests: PONYC_AMD_GUPS_SEG=n lists at most n chunks per segment, so that
+    // full segments send the rest through the streamers' own path)
+    const char* sg = getenv("PONYC_AMD_GUPS_SEG");
+    if(sg && atoi(sg) > 0) e.gups_seg = std::min<uint32_t>(e.gups_seg, (uint32_t)atoi(sg));
+  }
+  e.gups_l = (uint32_t)L; e.gups_parts = (uint32_t)parts;
   e.gups_type = t_def;
   g.gups_type = t_def;
   return 0;

@@ -99,6 +99,17 @@ def test_gups_chunks(engine_factory, oracle, monkeypatch, defer, logtable, updat
         assert d["gups_updates"] == 0
 
 
+def test_gups_list_full(engine_factory, oracle, monkeypatch):
+    """Segments of k_gups_apply's list held to 2 chunks (PONYC_AMD_GUPS_SEG):
+    the chunks past them are applied by their streamers in the same step,
+    every update issued — one step mixes both paths, still bit-exact."""
+    monkeypatch.setenv("PONYC_AMD_GUPS_SEG", "2")
+    g, o = _both(engine_factory, oracle, lambda e: W.gups(e, 12, 4, 1000, 64, 5), W.gups_result)
+    _assert_same(g, o)
+    d = g[1]["debug"]
+    assert 0 < d["gups_updates"] < 1000 * 64 * 6
+
+
 def test_storm(engine_factory, oracle):
     g, o = _both(engine_factory, oracle, lambda e: W.storm(e, 3000, 4, 12), lambda e, w: e.state_read(w["type"]))
     _assert_same(g, o)
