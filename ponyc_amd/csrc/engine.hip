@@ -2900,8 +2900,10 @@ int run_locked(uint64_t max_steps, uint64_t* steps_done)
       }
       uint32_t k = kChunk;
       if(max_steps) k = (uint32_t)std::min<uint64_t>(k, max_steps - done);
-      // pend[j] = pending at the start of step j (k_step), pend[k] = after the chunk
-      rc = pend_clear(0, k + 1);
+      // pend[j] = pending at the start of step j (k_step), pend[k] = after the
+      // chunk, pend[k + 1] the spill status below (its shards cleared too: a
+      // run_fixed before may have added to them)
+      rc = pend_clear(0, k + 2);
       if(rc) return rc;
       for(uint32_t j = 0; j < k; ++j)
       {
@@ -3040,9 +3042,14 @@ GPU_ACTOR_API int gpu_actor_run_fixed(uint64_t n)
   double ms_total = 0.0;
   while(left)
   {
-    // only the slots these launches add to (slot kPendPre is written whole)
-    rc = pend_clear(0, (uint32_t)std::min<uint64_t>(left, kPendPre));
-    if(rc) return rc;
+    // only the slots these launches add to (slot kPendPre is written whole);
+    // one rank reads none of them here (its spill status decides), and every
+    // reader of a slot clears it first (run, pending_now), so none at all
+    if(R() > 1)
+    {
+      rc = pend_clear(0, (uint32_t)std::min<uint64_t>(left, kPendPre));
+      if(rc) return rc;
+    }
     const uint32_t par0 = g.par, sidx0 = g.sidx;
     HIPCK(hipEventRecord(g.ev[0], g.stream));
     for(uint64_t j = 0; j < left; ++j)

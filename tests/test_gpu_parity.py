@@ -110,6 +110,26 @@ def test_gups_list_full(engine_factory, oracle, monkeypatch):
     assert 0 < d["gups_updates"] < 1000 * 64 * 6
 
 
+def test_run_fixed_then_run(engine_factory, oracle):
+    """run_fixed's steps then run to quiescence: run's per-step pending slots
+    and its spill-status slot start clean whatever run_fixed left in them."""
+    e = engine_factory()
+    w = W.ubench(e, 4096, 4, det=True, hops=60)
+    e.run_fixed(25)
+    e.run_fixed(7)
+    s = e.run(0)
+    ce = e.counts()
+    re = W.ubench_result(e, w)
+    wo = W.ubench(oracle, 4096, 4, det=True, hops=60)
+    so = oracle.run(0)
+    co = oracle.counts()
+    ro = W.ubench_result(oracle, wo)
+    assert 32 + s == so
+    np.testing.assert_array_equal(re, ro)
+    assert ce["delivered"] == co["delivered"] and ce["pending"] == co["pending"] == 0
+    assert e.debug_info()["fixups"] == 0
+
+
 def test_storm(engine_factory, oracle):
     g, o = _both(engine_factory, oracle, lambda e: W.storm(e, 3000, 4, 12), lambda e, w: e.state_read(w["type"]))
     _assert_same(g, o)
